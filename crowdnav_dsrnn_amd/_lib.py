@@ -1,0 +1,63 @@
+"""ctypes binding of the native HIP library (include/crowdnav.h).
+
+The product path has NO fallback: if lib/libcrowdnav_hip.so is missing or fails to load, every entry
+point raises. Build it with `python -m crowdnav_dsrnn_amd.build` (or __graft_entry__.build()).
+"""
+import ctypes
+import os
+
+from . import abi
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libcrowdnav_hip.so")
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryMissing(
+            "HIP engine library not built: %s is missing (run `python -m crowdnav_dsrnn_amd.build`)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    cfgp = ctypes.POINTER(abi.CnConfig)
+    L.cn_last_error.restype = ctypes.c_char_p
+    L.cn_version.restype = ctypes.c_char_p
+    L.cn_config_validate.argtypes = [cfgp]
+    L.cn_create.argtypes = [cfgp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.cn_destroy.argtypes = [vp]
+    L.cn_destroy.restype = None
+    L.cn_reset.argtypes = [vp, vp, vp, vp, vp]
+    L.cn_step.argtypes = [vp, vp, vp] + [vp] * 10
+    L.cn_state_bytes.argtypes = [vp, ctypes.POINTER(i64)]
+    L.cn_state_layout_offsets.argtypes = [cfgp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    L.cn_state_field_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int),
+                                      ctypes.POINTER(ctypes.c_int)]
+    L.cn_get_state.argtypes = [vp, vp, vp, ctypes.c_int]
+    L.cn_set_state.argtypes = [vp, vp, vp, ctypes.c_int]
+    L.cn_state_device_ptr.argtypes = [vp]
+    L.cn_state_device_ptr.restype = vp
+    L.cn_edge_features.argtypes = [vp, i64, ctypes.c_int] + [vp] * 14
+    for f in ("cn_config_validate", "cn_create", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
+              "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features"):
+        getattr(L, f).restype = i32
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError("crowdnav native error %d: %s" % (rc, lib().cn_last_error().decode()))
+    return rc
+
+
+EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "cn_destroy", "cn_reset", "cn_step",
+            "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
+            "cn_state_device_ptr", "cn_edge_features"]

@@ -1,0 +1,1602 @@
+// cn_engine.hip — MI355X (gfx950) batched CrowdSimDict engine: kernels + C ABI (include/crowdnav.h).
+//
+// Hot path per cn_step (one HIP stream, no host synchronisation):
+//   1. hipMemsetAsync(work_count)            — per-step RNG worklist reset (4 bytes)
+//   2. cn_step_kernel   (kernel A)           — one lane per (env, human), 256-lane workgroups holding
+//                                              floor(256/N) whole envs: SRNN.clip_action, the human
+//                                              policies (ORCA LP / social force) on the PRE-move state,
+//                                              calc_reward, kinematics, observation, Monitor; envs that
+//                                              need random numbers (reset, goal changes) are appended
+//                                              to a device worklist.
+//   3. cn_rng_kernel    (kernel B)           — one wave per listed env: numpy-legacy MT19937 in LDS,
+//                                              update_human_goals_randomly / update_human_goal, and the
+//                                              VecEnv auto-reset (CrowdSimDict.reset: reseed + spawn +
+//                                              first observation).
+// Reference: crowd_sim/envs/crowd_sim_dict.py:105-271, crowd_sim/envs/crowd_sim.py:296-1161,
+// crowd_sim/envs/utils/agent.py:172-218, crowd_nav/policy/{orca,social_force,srnn}.py; RVO2 v2.0
+// (third-party) restated in float32. Numerics: see cn_math.h.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/crowdnav.h"
+#include "../../include/crowdnav_state.h"
+#include "cn_math.h"
+
+using namespace cn;
+
+#define CN_BLK 256
+#define CN_MAX_A 32
+#define CN_DUMMY_POS 7.0
+
+// ------------------------------------------------------------------------------------------------
+// launch geometry + LDS plan of kernel A
+// ------------------------------------------------------------------------------------------------
+struct StepPlan {
+    int EPB;     // envs per workgroup
+    int M;       // observed slots per human (ORCA lines upper bound)
+    int A;       // agents per RVO2 simulator
+    int kd;      // A > 10: KdTree ordering needed
+    // LDS byte offsets
+    int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_lines, o_nd, o_ns, o_perm, total;
+};
+
+#define CN_RENV_F 14   // robot/env doubles per env in LDS
+#define CN_HUM_F 9     // human doubles per lane in LDS
+
+__host__ __device__ inline int cn_align16(int x) { return (x + 15) & ~15; }
+
+__host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
+{
+    StepPlan p;
+    p.EPB = CN_BLK / N;
+    p.A = N + (robot_visible ? 1 : 0);
+    p.M = p.A - 1;
+    p.kd = p.A > 10;
+    const int T = CN_BLK;
+    int o = 0;
+    p.o_renv = o;  o = cn_align16(o + CN_RENV_F * p.EPB * 8);
+    p.o_racts = o; o = cn_align16(o + 2 * p.EPB * 4);
+    p.o_rflag = o; o = cn_align16(o + 2 * p.EPB * 4);
+    p.o_rvr = o;   o = cn_align16(o + 8 * p.EPB * 8);
+    p.o_hum = o;   o = cn_align16(o + CN_HUM_F * T * 8);
+    p.o_lane = o;  o = cn_align16(o + T * 8 + T * 4);      // closest distance (f64) + flag word
+    p.o_orad = o;  o = cn_align16(o + T * 4);
+    p.o_lines = o; o = cn_align16(o + (p.M > 0 ? p.M : 1) * T * 16);
+    p.o_nd = o;    o = cn_align16(o + (p.M > 0 ? p.M : 1) * T * 4);
+    p.o_ns = o;    o = cn_align16(o + (p.M > 0 ? p.M : 1) * T);
+    p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * T : 0));
+    p.total = o;
+    return p;
+}
+
+// kernel-A LDS views
+struct SL {
+    double *r;        // [CN_RENV_F][EPB]
+    float *act;       // [2][EPB] clipped action (holonomic vx,vy / unicycle v,r)
+    uint32_t *rflag;  // [EPB] flags ; [EPB] aux
+    double *rvr;      // [8][EPB] robot VelocityRectangle corners
+    double *h;        // [CN_HUM_F][T]
+    double *cd;       // [T]
+    uint32_t *lf;     // [T]
+    float *orad;      // [T]
+    float4 *lines;    // [M][T]
+    float *nd;        // [M][T]
+    uint8_t *ns;      // [M][T]
+    uint8_t *perm;    // [A][T]
+};
+enum { R_PX, R_PY, R_GX, R_GY, R_VX, R_VY, R_TH, R_RAD, R_VP, R_POT, R_GT, R_DV, R_NX, R_NY };
+enum { H_PX, H_PY, H_GX, H_GY, H_VX, H_VY, H_R, H_VP, H_TH };
+#define RF(sl, f, el, EPB) ((sl).r[(f) * (EPB) + (el)])
+#define HF(sl, f, t) ((sl).h[(f) * CN_BLK + (t)])
+
+// lane flag bits
+#define LF_VR 1u
+#define LF_NOTREACHED 2u
+#define LF_ENDGOAL 4u
+
+// ------------------------------------------------------------------------------------------------
+// FOV (CrowdSim.detect_visible, crowd_sim.py:820-847)
+// ------------------------------------------------------------------------------------------------
+// unit FOV direction of an agent with float64 heading
+__device__ inline void fov_dir64(double th, double &fx, double &fy)
+{
+    fx = cos(th); fy = sin(th);
+    const double nf = np_norm2(fx, fy);
+    fx = ddiv(fx, nf); fy = ddiv(fy, nf);
+}
+// float32 heading (np.float32 robot state): float32 cos/sin/norm, promoted for the dot
+__device__ inline void fov_dir32(float th, double &fx, double &fy)
+{
+    float cx = np_cosf(th), cy = np_sinf(th);
+    const float nf = np_norm2f(cx, cy);
+    fx = (double)fdiv(cx, nf); fy = (double)fdiv(cy, nf);
+}
+__device__ inline bool in_fov(double fx, double fy, double px1, double py1, double px2, double py2, double fov)
+{
+    double vx = px2 - px1, vy = py2 - py1;
+    const double nv = np_norm2(vx, vy);
+    vx = ddiv(vx, nv); vy = ddiv(vy, nv);
+    double d = np_dot2(fx, fy, vx, vy);
+    if (d != d) return false;  // coincident agents: arccos(nan) -> not visible
+    if (fov >= 2.0 * CN_PI) return true;
+    d = d < -1.0 ? -1.0 : (d > 1.0 ? 1.0 : d);
+    return fabs(acos(d)) <= fov / 2;
+}
+
+// ------------------------------------------------------------------------------------------------
+// shapely restatements (parity unpinned)
+// ------------------------------------------------------------------------------------------------
+__device__ inline void vel_rect(double px, double py, double vx, double vy, double r, bool f32, double *cx,
+                                double *cy)
+{
+    const double w = 2 * r * 1;
+    double len, dth, xos, yos;
+    if (f32) {
+        const float fvx = (float)vx, fvy = (float)vy;
+        len = (double)(3.0f * fsqrt(fvx * fvx + fvy * fvy));
+        const float h = atan2f(fvy, fvx);
+        dth = (double)(h - (float)(CN_PI / 2));
+        xos = px + (double)((float)r * np_cosf(h));
+        yos = py + (double)((float)r * np_sinf(h));
+    } else {
+        len = 3 * dsqrt(vx * vx + vy * vy);
+        const double heading = atan2(vy, vx);
+        dth = heading - CN_PI / 2;
+        xos = px + r * cos(heading);
+        yos = py + r * sin(heading);
+    }
+    double c = cos(dth), s = sin(dth);
+    if (fabs(c) < 2.5e-16) c = 0.0;
+    if (fabs(s) < 2.5e-16) s = 0.0;
+    const double bx[4] = {w / 2, w / 2, -w / 2, -w / 2};
+    const double by0[4] = {-len / 2, len / 2, len / 2, -len / 2};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double x = bx[k], y = by0[k] + len / 2;
+        cx[k] = (c * x - s * y) + xos;
+        cy[k] = (s * x + c * y) + yos;
+    }
+}
+
+__device__ inline bool quads_intersect(const double *ax, const double *ay, const double *bx, const double *by)
+{
+    for (int p = 0; p < 2; ++p) {
+        const double *qx = p ? bx : ax, *qy = p ? by : ay;
+        for (int k = 0; k < 4; ++k) {
+            const double ex = qx[(k + 1) & 3] - qx[k], ey = qy[(k + 1) & 3] - qy[k];
+            if (ex == 0.0 && ey == 0.0) continue;
+            for (int t = 0; t < 2; ++t) {
+                const double nx = t ? ex : -ey, ny = t ? ey : ex;
+                double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const double pa = ax[v] * nx + ay[v] * ny, pb = bx[v] * nx + by[v] * ny;
+                    amin = pa < amin ? pa : amin; amax = pa > amax ? pa : amax;
+                    bmin = pb < bmin ? pb : bmin; bmax = pb > bmax ? pb : bmax;
+                }
+                if (amax < bmin || bmax < amin) return false;
+            }
+        }
+    }
+    return true;
+}
+
+__device__ inline bool inside_world(double px, double py, double r, double half)
+{
+    const bool right = (px + r >= half) && (px - r <= half);
+    const bool left = (px - r <= -half) && (px + r >= -half);
+    const bool top = (py + r >= half) && (py - r <= half);
+    const bool bottom = (py - r <= -half) && (py + r >= -half);
+    return !(right || left || top || bottom);
+}
+
+__device__ inline void norm_zone(double px, double py, double vx, double vy, double r, bool f32, int lhs, int left,
+                                 double *cx, double *cy)
+{
+    const double w = 2 * r * 1.5, len = 1.5 * 1.2;
+    double dth, xos, yos;
+    if (f32) {
+        const float h = atan2f((float)vy, (float)vx);
+        dth = (double)(h - (float)(CN_PI / 2));
+        xos = px + (double)((float)r * np_cosf(h));
+        yos = py + (double)((float)r * np_sinf(h));
+    } else {
+        const double heading = atan2(vy, vx);
+        dth = heading - CN_PI / 2;
+        xos = px + r * cos(heading);
+        yos = py + r * sin(heading);
+    }
+    double tx, ty;
+    if (lhs) { if (left) { tx = -w / 2; ty = len / 2 + 0.6; } else { tx = w / 2; ty = len / 2; } }
+    else { if (left) { tx = -w / 2; ty = len / 2; } else { tx = w / 2; ty = len / 2 + 0.6; } }
+    double c = cos(dth), s = sin(dth);
+    if (fabs(c) < 2.5e-16) c = 0.0;
+    if (fabs(s) < 2.5e-16) s = 0.0;
+    const double bx[4] = {w / 2, w / 2, -w / 2, -w / 2};
+    const double by[4] = {-len / 2, len / 2, len / 2, -len / 2};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const double x = bx[k] + tx, y = by[k] + ty;
+        cx[k] = (c * x - s * y) + xos;
+        cy[k] = (s * x + c * y) + yos;
+    }
+}
+
+// robot disc (GEOS 64-gon buffer) vs convex quad; unit circle table precomputed on the host
+__constant__ double c_circ_cos[64];
+__constant__ double c_circ_sin[64];
+
+__device__ inline bool disc_quad_intersect(double px, double py, double r, const double *qx, const double *qy)
+{
+    double vx[64], vy[64];
+    for (int k = 0; k < 64; ++k) { vx[k] = px + r * c_circ_cos[k]; vy[k] = py + r * c_circ_sin[k]; }
+    vx[0] = px + r; vy[0] = py;
+    for (int p = 0; p < 2; ++p) {
+        const int nv = p ? 64 : 4;
+        const double *ex_ = p ? vx : qx, *ey_ = p ? vy : qy;
+        for (int k = 0; k < nv; ++k) {
+            const double ex = ex_[(k + 1) % nv] - ex_[k], ey = ey_[(k + 1) % nv] - ey_[k];
+            if (ex == 0.0 && ey == 0.0) continue;
+            const double nx = -ey, ny = ex;
+            double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+            for (int v = 0; v < 64; ++v) { const double t = vx[v] * nx + vy[v] * ny; amin = t < amin ? t : amin; amax = t > amax ? t : amax; }
+            for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
+            if (amax < bmin || bmax < amin) return false;
+        }
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// RVO2 v2.0 agent-0 solve (float32) with ORCA lines in LDS ([line][lane] float4: point.xy, dir.xy)
+// ------------------------------------------------------------------------------------------------
+#define RVO_EPSILON 0.00001f
+
+struct LineView {
+    float4 *base;
+    int tid;
+    __device__ float4 operator[](int k) const { return base[k * CN_BLK + tid]; }
+    __device__ void set(int k, float4 v) const { base[k * CN_BLK + tid] = v; }
+};
+
+__device__ inline float det2(float ax, float ay, float bx, float by) { return ax * by - ay * bx; }
+
+// linearProgram1 on plain lines
+__device__ bool lp1(const LineView &L, int no, float radius, float ox, float oy, bool dirOpt, float &rx, float &ry)
+{
+    const float4 ln = L[no];
+    const float dot = ln.x * ln.z + ln.y * ln.w;
+    const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
+    if (disc < 0.0f) return false;
+    const float sd = fsqrt(disc);
+    float tL = -dot - sd, tR = -dot + sd;
+    for (int i = 0; i < no; ++i) {
+        const float4 li = L[i];
+        const float den = det2(ln.z, ln.w, li.z, li.w);
+        const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
+        if (fabsf(den) <= RVO_EPSILON) {
+            if (num < 0.0f) return false;
+            continue;
+        }
+        const float t = fdiv(num, den);
+        if (den >= 0.0f) tR = (t < tR) ? t : tR;
+        else tL = (tL < t) ? t : tL;
+        if (tL > tR) return false;
+    }
+    if (dirOpt) {
+        if (ox * ln.z + oy * ln.w > 0.0f) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
+        else { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
+    } else {
+        const float t = ln.z * (ox - ln.x) + ln.w * (oy - ln.y);
+        if (t < tL) { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
+        else if (t > tR) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
+        else { rx = ln.x + t * ln.z; ry = ln.y + t * ln.w; }
+    }
+    return true;
+}
+
+__device__ int lp2(const LineView &L, int n, float radius, float ox, float oy, float &rx, float &ry)
+{
+    if (ox * ox + oy * oy > radius * radius) {
+        const float inv = fdiv(1.0f, fsqrt(ox * ox + oy * oy));
+        rx = (ox * inv) * radius; ry = (oy * inv) * radius;
+    } else { rx = ox; ry = oy; }
+    for (int i = 0; i < n; ++i) {
+        const float4 li = L[i];
+        if (det2(li.z, li.w, li.x - rx, li.y - ry) > 0.0f) {
+            const float tx = rx, ty = ry;
+            if (!lp1(L, i, radius, ox, oy, false, rx, ry)) { rx = tx; ry = ty; return i; }
+        }
+    }
+    return n;
+}
+
+// projected line j of LP3's line i (recomputed on the fly; `valid` false when skipped)
+__device__ inline float4 proj_line(const float4 li, const float4 lj, bool &valid)
+{
+    float4 r;
+    const float determinant = det2(li.z, li.w, lj.z, lj.w);
+    valid = true;
+    if (fabsf(determinant) <= RVO_EPSILON) {
+        if (li.z * lj.z + li.w * lj.w > 0.0f) { valid = false; return r; }
+        r.x = 0.5f * (li.x + lj.x);
+        r.y = 0.5f * (li.y + lj.y);
+    } else {
+        const float s = fdiv(det2(lj.z, lj.w, li.x - lj.x, li.y - lj.y), determinant);
+        r.x = li.x + s * li.z;
+        r.y = li.y + s * li.w;
+    }
+    const float ddx = lj.z - li.z, ddy = lj.w - li.w;
+    const float inv = fdiv(1.0f, fsqrt(ddx * ddx + ddy * ddy));
+    r.z = ddx * inv; r.w = ddy * inv;
+    return r;
+}
+
+// linearProgram1 (direction-optimal) over the projected lines of line `li` (lines < ii)
+__device__ bool lp1_proj(const LineView &L, int ii, int no, float radius, float ox, float oy, float &rx, float &ry)
+{
+    const float4 li = L[ii];
+    bool v;
+    const float4 ln = proj_line(li, L[no], v);
+    const float dot = ln.x * ln.z + ln.y * ln.w;
+    const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
+    if (disc < 0.0f) return false;
+    const float sd = fsqrt(disc);
+    float tL = -dot - sd, tR = -dot + sd;
+    for (int i = 0; i < no; ++i) {
+        bool vi;
+        const float4 pi = proj_line(li, L[i], vi);
+        if (!vi) continue;
+        const float den = det2(ln.z, ln.w, pi.z, pi.w);
+        const float num = det2(pi.z, pi.w, ln.x - pi.x, ln.y - pi.y);
+        if (fabsf(den) <= RVO_EPSILON) {
+            if (num < 0.0f) return false;
+            continue;
+        }
+        const float t = fdiv(num, den);
+        if (den >= 0.0f) tR = (t < tR) ? t : tR;
+        else tL = (tL < t) ? t : tL;
+        if (tL > tR) return false;
+    }
+    if (ox * ln.z + oy * ln.w > 0.0f) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
+    else { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
+    return true;
+}
+
+__device__ void lp3(const LineView &L, int n, int begin, float radius, float &rx, float &ry)
+{
+    float distance = 0.0f;
+    for (int i = begin; i < n; ++i) {
+        const float4 li = L[i];
+        if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
+            const float tx = rx, ty = ry;
+            // linearProgram2(projLines, radius, (-dir_i.y, dir_i.x), directionOpt = true)
+            const float ox = -li.w, oy = li.z;
+            rx = ox * radius; ry = oy * radius;
+            bool fail = false;
+            for (int j = 0; j < i && !fail; ++j) {
+                bool vj;
+                const float4 pj = proj_line(li, L[j], vj);
+                if (!vj) continue;
+                if (det2(pj.z, pj.w, pj.x - rx, pj.y - ry) > 0.0f) {
+                    const float sx = rx, sy = ry;
+                    if (!lp1_proj(L, i, j, radius, ox, oy, rx, ry)) { rx = sx; ry = sy; fail = true; }
+                }
+            }
+            if (fail) { rx = tx; ry = ty; }
+            distance = det2(li.z, li.w, li.x - rx, li.y - ry);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// kernel A
+// ------------------------------------------------------------------------------------------------
+struct StepArgs {
+    cn_state_ptrs s;
+    const float *actions;
+    float *robot_node, *temporal, *spatial;
+    float *reward;
+    uint8_t *done;
+    int8_t *event;
+    float *info;
+    double *ep_return;
+    int32_t *ep_len;
+    uint32_t *work;
+    uint32_t *work_count;
+    int E;
+};
+
+// observed agent of slot k seen by lane (human i of env base eb): position/velocity float32,
+// frozen RVO2 radius; `vis` = visible now, `dm` = dummy at simulator creation
+__device__ inline void slot_agent(const SL &sl, const cn_config &c, int eb, int el, int EPB, int N, int i, int k,
+                                  uint32_t vis, uint32_t dm, float rdummy, float &x, float &y, float &vx, float &vy,
+                                  float &r)
+{
+    const bool v = (vis >> k) & 1u;
+    if (k < N - 1) {
+        const int j = eb + (k < i ? k : k + 1);
+        if (v) {
+            x = (float)HF(sl, H_PX, j); y = (float)HF(sl, H_PY, j);
+            vx = (float)HF(sl, H_VX, j); vy = (float)HF(sl, H_VY, j);
+        } else { x = (float)CN_DUMMY_POS; y = (float)CN_DUMMY_POS; vx = 0.0f; vy = 0.0f; }
+        r = ((dm >> k) & 1u) ? rdummy : sl.orad[j];
+    } else {  // robot slot (robot.visible)
+        if (v) {
+            x = (float)RF(sl, R_PX, el, EPB); y = (float)RF(sl, R_PY, el, EPB);
+            vx = (float)RF(sl, R_VX, el, EPB); vy = (float)RF(sl, R_VY, el, EPB);
+        } else { x = (float)CN_DUMMY_POS; y = (float)CN_DUMMY_POS; vx = 0.0f; vy = 0.0f; }
+        r = ((dm >> k) & 1u) ? (float)(c.robot_radius + 0.01 + c.orca_safety_space)
+                             : (float)(RF(sl, R_RAD, el, EPB) + 0.01 + c.orca_safety_space);
+    }
+}
+
+// RVO2 Agent::insertAgentNeighbor into the lane's sorted (distSq, slot) list in LDS
+__device__ inline void insert_nbr(const SL &sl, int tid, int &cnt, int maxN, int slot, float distSq, float &rangeSq)
+{
+    if (distSq < rangeSq) {
+        if (cnt < maxN) ++cnt;
+        int q = cnt - 1;
+        while (q != 0 && distSq < sl.nd[(q - 1) * CN_BLK + tid]) {
+            sl.nd[q * CN_BLK + tid] = sl.nd[(q - 1) * CN_BLK + tid];
+            sl.ns[q * CN_BLK + tid] = sl.ns[(q - 1) * CN_BLK + tid];
+            --q;
+        }
+        sl.nd[q * CN_BLK + tid] = distSq;
+        sl.ns[q * CN_BLK + tid] = (uint8_t)slot;
+        if (cnt == maxN) rangeSq = sl.nd[(cnt - 1) * CN_BLK + tid];
+    }
+}
+
+__device__ inline float bbox_dist(float x, float y, float mnx, float mxx, float mny, float mxy)
+{
+    const float a = (0.0f < mnx - x) ? mnx - x : 0.0f, b = (0.0f < x - mxx) ? x - mxx : 0.0f;
+    const float cc = (0.0f < mny - y) ? mny - y : 0.0f, d = (0.0f < y - mxy) ? y - mxy : 0.0f;
+    return a * a + b * b + cc * cc + d * d;
+}
+
+__global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c)
+{
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int N = c.human_num;
+    const StepPlan P = cn_step_plan(N, c.robot_visible);
+    const int EPB = P.EPB, M = P.M, A = P.A;
+    SL sl;
+    sl.r = (double *)(smem + P.o_renv);
+    sl.act = (float *)(smem + P.o_racts);
+    sl.rflag = (uint32_t *)(smem + P.o_rflag);
+    sl.rvr = (double *)(smem + P.o_rvr);
+    sl.h = (double *)(smem + P.o_hum);
+    sl.cd = (double *)(smem + P.o_lane);
+    sl.lf = (uint32_t *)(smem + P.o_lane + CN_BLK * 8);
+    sl.orad = (float *)(smem + P.o_orad);
+    sl.lines = (float4 *)(smem + P.o_lines);
+    sl.nd = (float *)(smem + P.o_nd);
+    sl.ns = (uint8_t *)(smem + P.o_ns);
+    sl.perm = (uint8_t *)(smem + P.o_perm);
+    const cn_state_ptrs &S = g.s;
+
+    const int tid = threadIdx.x;
+    const int e0 = blockIdx.x * EPB;
+    const int nenv_here = min(EPB, g.E - e0);
+    const int el = tid / N, i = tid - el * N;
+    const bool hl = el < nenv_here;               // human lane
+    const int64_t gh = (int64_t)(e0 + el) * N + i;  // global human index
+    const bool rl = tid < nenv_here;              // env lane (robot / reward / bookkeeping)
+    const int64_t ge = e0 + tid;
+    const bool holo = c.kinematics == CN_HOLONOMIC;
+    const double dt = c.time_step;
+
+    // ---- phase 0: load state into LDS -----------------------------------------------------------
+    double bpx = 0, bpy = 0, bvx = 0, bvy = 0, br = 0;
+    if (hl) {
+        HF(sl, H_PX, tid) = S.h_px[gh]; HF(sl, H_PY, tid) = S.h_py[gh];
+        HF(sl, H_GX, tid) = S.h_gx[gh]; HF(sl, H_GY, tid) = S.h_gy[gh];
+        HF(sl, H_VX, tid) = S.h_vx[gh]; HF(sl, H_VY, tid) = S.h_vy[gh];
+        HF(sl, H_R, tid) = S.h_r[gh]; HF(sl, H_VP, tid) = S.h_vpref[gh];
+        HF(sl, H_TH, tid) = S.h_theta[gh];
+        bpx = S.b_px[gh]; bpy = S.b_py[gh]; bvx = S.b_vx[gh]; bvy = S.b_vy[gh]; br = S.b_r[gh];
+    }
+    if (rl) {
+        RF(sl, R_PX, tid, EPB) = S.r_px[ge]; RF(sl, R_PY, tid, EPB) = S.r_py[ge];
+        RF(sl, R_GX, tid, EPB) = S.r_gx[ge]; RF(sl, R_GY, tid, EPB) = S.r_gy[ge];
+        RF(sl, R_VX, tid, EPB) = S.r_vx[ge]; RF(sl, R_VY, tid, EPB) = S.r_vy[ge];
+        RF(sl, R_TH, tid, EPB) = S.r_theta[ge]; RF(sl, R_RAD, tid, EPB) = S.r_radius[ge];
+        RF(sl, R_VP, tid, EPB) = S.r_vpref[ge]; RF(sl, R_POT, tid, EPB) = S.potential[ge];
+        RF(sl, R_GT, tid, EPB) = S.gtime[ge]; RF(sl, R_DV, tid, EPB) = S.r_dv[ge];
+        sl.rflag[tid] = S.flags[ge];
+        // ---- SRNN.clip_action (srnn.py:18-48) + unicycle integrator (crowd_sim_dict.py:211-217)
+        float a0 = g.actions[ge * 2], a1 = g.actions[ge * 2 + 1];
+        if (holo) {
+            const float n = np_norm2f(a0, a1);
+            if ((double)n > RF(sl, R_VP, tid, EPB)) {
+                const float vp = (float)RF(sl, R_VP, tid, EPB);
+                a0 = fdiv(a0, n) * vp; a1 = fdiv(a1, n) * vp;
+            }
+        } else {
+            a0 = np_clipf(a0, -0.1f, 0.1f);
+            a1 = np_clipf(a1, -0.1f, 0.1f);
+            const float vp = (float)RF(sl, R_VP, tid, EPB);
+            const float dv = np_clipf((float)RF(sl, R_DV, tid, EPB) + a0, -vp, vp);
+            RF(sl, R_DV, tid, EPB) = dv;
+            a0 = dv;
+        }
+        sl.act[tid] = a0; sl.act[EPB + tid] = a1;
+        // robot VelocityRectangle (pre-move)
+        double cx[4], cy[4];
+        vel_rect(RF(sl, R_PX, tid, EPB), RF(sl, R_PY, tid, EPB), RF(sl, R_VX, tid, EPB), RF(sl, R_VY, tid, EPB),
+                 RF(sl, R_RAD, tid, EPB), (sl.rflag[tid] & CN_FLAG_ROBOT_F32) != 0, cx, cy);
+        for (int k = 0; k < 4; ++k) { sl.rvr[k * EPB + tid] = cx[k]; sl.rvr[(4 + k) * EPB + tid] = cy[k]; }
+    }
+    __syncthreads();
+
+    // ---- phase 1: visibility of the other agents to human i, frozen simulator parameters --------
+    const bool orca = c.human_policy == CN_POLICY_ORCA;
+    uint32_t vis = 0, dm = 0;
+    float my_vmax = 0.0f;
+    bool frozen = true;
+    if (hl) {
+        const int eb = el * N;
+        double fx, fy;
+        if (holo) fov_dir64(atan2(HF(sl, H_VY, tid), HF(sl, H_VX, tid)), fx, fy);
+        else fov_dir64(HF(sl, H_TH, tid), fx, fy);
+        const double px = HF(sl, H_PX, tid), py = HF(sl, H_PY, tid);
+        for (int k = 0; k < N - 1; ++k) {
+            const int j = eb + (k < i ? k : k + 1);
+            if (in_fov(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov)) vis |= 1u << k;
+        }
+        if (c.robot_visible && in_fov(fx, fy, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB), c.human_fov))
+            vis |= 1u << (N - 1);
+        if (orca) {
+            frozen = (sl.rflag[el] & CN_FLAG_ORCA_FROZEN) != 0;
+            if (frozen) {
+                sl.orad[tid] = S.o_r[gh];
+                my_vmax = S.o_vmax[gh];
+                dm = S.o_dmask[gh];
+            } else {  // first ORCA.predict of the episode creates the simulator (orca.py:85-109)
+                sl.orad[tid] = (float)(HF(sl, H_R, tid) + 0.01 + c.orca_safety_space);
+                my_vmax = (float)HF(sl, H_VP, tid);
+                dm = ~vis & ((M >= 32) ? 0xffffffffu : ((1u << M) - 1u));
+                S.o_r[gh] = sl.orad[tid];
+                S.o_vmax[gh] = my_vmax;
+                S.o_dmask[gh] = dm;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- phase 2: human policy (PRE-move state) + per-human reward terms -------------------------
+    double nvx = 0.0, nvy = 0.0;
+    if (hl) {
+        const int eb = el * N;
+        const double px = HF(sl, H_PX, tid), py = HF(sl, H_PY, tid);
+        const double vx0 = HF(sl, H_VX, tid), vy0 = HF(sl, H_VY, tid);
+        const double rad = HF(sl, H_R, tid), vpref = HF(sl, H_VP, tid);
+        if (orca) {
+            const float rdummy = (float)(c.human_radius + 0.01 + c.orca_safety_space);
+            const float X0 = (float)px, Y0 = (float)py, VX0 = (float)vx0, VY0 = (float)vy0;
+            const float R0 = sl.orad[tid];
+            float rangeSq = (float)c.orca_neighbor_dist * (float)c.orca_neighbor_dist;
+            int cnt = 0;
+            const int maxN = M;
+            if (maxN > 0) {
+                if (!P.kd) {
+                    for (int k = 0; k < M; ++k) {
+                        float x, y, vx, vy, r;
+                        slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, x, y, vx, vy, r);
+                        const float dx = X0 - x, dy = Y0 - y;
+                        insert_nbr(sl, tid, cnt, maxN, k, dx * dx + dy * dy, rangeSq);
+                    }
+                } else {
+                    // KdTree: persisted agents_ order (identity at simulator creation)
+                    uint8_t *perm = sl.perm;
+                    for (int a = 0; a < A; ++a)
+                        perm[a * CN_BLK + tid] = frozen ? S.o_perm[gh * A + a] : (uint8_t)a;
+                    auto AX = [&](int a) -> float {
+                        if (a == 0) return X0;
+                        float x, y, vx, vy, r;
+                        slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
+                        return x;
+                    };
+                    auto AY = [&](int a) -> float {
+                        if (a == 0) return Y0;
+                        float x, y, vx, vy, r;
+                        slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
+                        return y;
+                    };
+                    // build (buildAgentTreeRecursive), iteratively; partitions perm in place
+                    int stb[CN_MAX_A], ste[CN_MAX_A], sp = 0;
+                    stb[sp] = 0; ste[sp] = A; ++sp;
+                    while (sp > 0) {
+                        --sp;
+                        const int b = stb[sp], e = ste[sp];
+                        if (e - b <= 10) continue;
+                        float mnx = AX(perm[b * CN_BLK + tid]), mxx = mnx;
+                        float mny = AY(perm[b * CN_BLK + tid]), mxy = mny;
+                        for (int q = b + 1; q < e; ++q) {
+                            const int a = perm[q * CN_BLK + tid];
+                            const float x = AX(a), y = AY(a);
+                            mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
+                            mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
+                        }
+                        const bool vert = (mxx - mnx > mxy - mny);
+                        const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
+                        int left = b, right = e;
+                        while (left < right) {
+                            while (left < right) {
+                                const int a = perm[left * CN_BLK + tid];
+                                if (!((vert ? AX(a) : AY(a)) < split)) break;
+                                ++left;
+                            }
+                            while (right > left) {
+                                const int a = perm[(right - 1) * CN_BLK + tid];
+                                if (!((vert ? AX(a) : AY(a)) >= split)) break;
+                                --right;
+                            }
+                            if (left < right) {
+                                const uint8_t t0 = perm[left * CN_BLK + tid];
+                                perm[left * CN_BLK + tid] = perm[(right - 1) * CN_BLK + tid];
+                                perm[(right - 1) * CN_BLK + tid] = t0;
+                                ++left; --right;
+                            }
+                        }
+                        if (left == b) { ++left; }
+                        stb[sp] = b; ste[sp] = left; ++sp;
+                        stb[sp] = left; ste[sp] = e; ++sp;
+                    }
+                    for (int a = 0; a < A; ++a) S.o_perm[gh * A + a] = perm[a * CN_BLK + tid];
+                    // query (queryAgentTreeRecursive): closer child first, ties -> right; subtree
+                    // pruning never drops an in-range agent, so visiting every leaf is equivalent
+                    sp = 0; stb[sp] = 0; ste[sp] = A; ++sp;
+                    while (sp > 0) {
+                        --sp;
+                        const int b = stb[sp], e = ste[sp];
+                        if (e - b <= 10) {
+                            for (int q = b; q < e; ++q) {
+                                const int a = perm[q * CN_BLK + tid];
+                                if (a == 0) continue;
+                                const float dx = X0 - AX(a), dy = Y0 - AY(a);
+                                insert_nbr(sl, tid, cnt, maxN, a - 1, dx * dx + dy * dy, rangeSq);
+                            }
+                            continue;
+                        }
+                        float mnx = AX(perm[b * CN_BLK + tid]), mxx = mnx;
+                        float mny = AY(perm[b * CN_BLK + tid]), mxy = mny;
+                        for (int q = b + 1; q < e; ++q) {
+                            const int a = perm[q * CN_BLK + tid];
+                            const float x = AX(a), y = AY(a);
+                            mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
+                            mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
+                        }
+                        const bool vert = (mxx - mnx > mxy - mny);
+                        const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
+                        int left = b;
+                        for (int q = b; q < e; ++q) {
+                            const int a = perm[q * CN_BLK + tid];
+                            if ((vert ? AX(a) : AY(a)) < split) ++left;
+                        }
+                        if (left == b) ++left;
+                        float bb[2][4];
+                        for (int ch = 0; ch < 2; ++ch) {
+                            const int cb = ch ? left : b, ce = ch ? e : left;
+                            float a0x = AX(perm[cb * CN_BLK + tid]), a1x = a0x;
+                            float a0y = AY(perm[cb * CN_BLK + tid]), a1y = a0y;
+                            for (int q = cb + 1; q < ce; ++q) {
+                                const int a = perm[q * CN_BLK + tid];
+                                const float x = AX(a), y = AY(a);
+                                a1x = a1x < x ? x : a1x; a0x = x < a0x ? x : a0x;
+                                a1y = a1y < y ? y : a1y; a0y = y < a0y ? y : a0y;
+                            }
+                            bb[ch][0] = a0x; bb[ch][1] = a1x; bb[ch][2] = a0y; bb[ch][3] = a1y;
+                        }
+                        const float dl = bbox_dist(X0, Y0, bb[0][0], bb[0][1], bb[0][2], bb[0][3]);
+                        const float dr = bbox_dist(X0, Y0, bb[1][0], bb[1][1], bb[1][2], bb[1][3]);
+                        if (dl < dr) {  // visit left first: push right, then left
+                            stb[sp] = left; ste[sp] = e; ++sp; stb[sp] = b; ste[sp] = left; ++sp;
+                        } else {
+                            stb[sp] = b; ste[sp] = left; ++sp; stb[sp] = left; ste[sp] = e; ++sp;
+                        }
+                    }
+                }
+            }
+            // ORCA lines (Agent::computeNewVelocity, agents only)
+            LineView L{sl.lines, tid};
+            const float invTH = fdiv(1.0f, (float)c.orca_time_horizon);
+            for (int p = 0; p < cnt; ++p) {
+                const int k = sl.ns[p * CN_BLK + tid];
+                float ox, oy, ovx, ovy, orr;
+                slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, ox, oy, ovx, ovy, orr);
+                const float rpx = ox - X0, rpy = oy - Y0;
+                const float rvx = VX0 - ovx, rvy = VY0 - ovy;
+                const float distSq = rpx * rpx + rpy * rpy;
+                const float cr = R0 + orr;
+                const float crSq = cr * cr;
+                float ux, uy, dx, dy;
+                if (distSq > crSq) {
+                    const float wx = rvx - invTH * rpx, wy = rvy - invTH * rpy;
+                    const float wLenSq = wx * wx + wy * wy;
+                    const float dot1 = wx * rpx + wy * rpy;
+                    if (dot1 < 0.0f && dot1 * dot1 > crSq * wLenSq) {
+                        const float wLen = fsqrt(wLenSq);
+                        const float inv = fdiv(1.0f, wLen);
+                        const float uwx = wx * inv, uwy = wy * inv;
+                        dx = uwy; dy = -uwx;
+                        const float s = cr * invTH - wLen;
+                        ux = s * uwx; uy = s * uwy;
+                    } else {
+                        const float leg = fsqrt(distSq - crSq);
+                        const float inv = fdiv(1.0f, distSq);
+                        if (det2(rpx, rpy, wx, wy) > 0.0f) {
+                            dx = (rpx * leg - rpy * cr) * inv;
+                            dy = (rpx * cr + rpy * leg) * inv;
+                        } else {
+                            dx = -((rpx * leg + rpy * cr) * inv);
+                            dy = -((-rpx * cr + rpy * leg) * inv);
+                        }
+                        const float dot2 = rvx * dx + rvy * dy;
+                        ux = dot2 * dx - rvx; uy = dot2 * dy - rvy;
+                    }
+                } else {
+                    const float invTS = fdiv(1.0f, (float)dt);
+                    const float wx = rvx - invTS * rpx, wy = rvy - invTS * rpy;
+                    const float wLen = fsqrt(wx * wx + wy * wy);
+                    const float inv = fdiv(1.0f, wLen);
+                    const float uwx = wx * inv, uwy = wy * inv;
+                    dx = uwy; dy = -uwx;
+                    const float s = cr * invTS - wLen;
+                    ux = s * uwx; uy = s * uwy;
+                }
+                L.set(p, make_float4(VX0 + 0.5f * ux, VY0 + 0.5f * uy, dx, dy));
+            }
+            // preferred velocity: unit vector to the goal only if farther than 1 (orca.py:118-122)
+            double gdx = HF(sl, H_GX, tid) - px, gdy = HF(sl, H_GY, tid) - py;
+            const double speed = np_norm2(gdx, gdy);
+            if (speed > 1.0) { gdx = ddiv(gdx, speed); gdy = ddiv(gdy, speed); }
+            float rx, ry;
+            const int fail_at = lp2(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
+            if (fail_at < cnt) lp3(L, cnt, fail_at, my_vmax, rx, ry);
+            nvx = (double)rx; nvy = (double)ry;
+        } else {
+            // SOCIAL_FORCE.predict (social_force.py:11-66)
+            const double dx = HF(sl, H_GX, tid) - px, dy = HF(sl, H_GY, tid) - py;
+            const double dist = dsqrt(dx * dx + dy * dy);
+            const double dvx = ddiv(dx, dist) * vpref, dvy = ddiv(dy, dist) * vpref;
+            const double cdx = c.sf_KI * (dvx - vx0), cdy = c.sf_KI * (dvy - vy0);
+            double ix = 0.0, iy = 0.0;
+            for (int k = 0; k < M; ++k) {
+                double ox, oy, orr;
+                const bool v = (vis >> k) & 1u;
+                if (k < N - 1) {
+                    const int j = eb + (k < i ? k : k + 1);
+                    ox = v ? HF(sl, H_PX, j) : CN_DUMMY_POS; oy = v ? HF(sl, H_PY, j) : CN_DUMMY_POS;
+                    orr = v ? HF(sl, H_R, j) : c.human_radius;
+                } else {
+                    ox = v ? RF(sl, R_PX, el, EPB) : CN_DUMMY_POS; oy = v ? RF(sl, R_PY, el, EPB) : CN_DUMMY_POS;
+                    orr = v ? RF(sl, R_RAD, el, EPB) : c.robot_radius;
+                }
+                const double ddx = px - ox, ddy = py - oy;
+                const double d = dsqrt(ddx * ddx + ddy * ddy);
+                const double ex = exp(ddiv(rad + orr - d, c.sf_B));
+                ix += c.sf_A * ex * ddiv(ddx, d);
+                iy += c.sf_A * ex * ddiv(ddy, d);
+            }
+            const double tx = (cdx + ix) * dt, ty = (cdy + iy) * dt;
+            const double nx = vx0 + tx, ny = vy0 + ty;
+            const double n = np_norm2(nx, ny);
+            if (n > vpref) { nvx = ddiv(nx, n) * vpref; nvy = ddiv(ny, n) * vpref; }
+            else { nvx = nx; nvy = ny; }
+        }
+        // per-human terms of calc_reward (crowd_sim.py:934-969), PRE-move
+        const double rdx = px - RF(sl, R_PX, el, EPB), rdy = py - RF(sl, R_PY, el, EPB);
+        sl.cd[tid] = dsqrt(rdx * rdx + rdy * rdy) - rad - RF(sl, R_RAD, el, EPB);
+        double hcx[4], hcy[4], rcx[4], rcy[4];
+        vel_rect(px, py, vx0, vy0, rad, false, hcx, hcy);
+        for (int k = 0; k < 4; ++k) { rcx[k] = sl.rvr[k * EPB + el]; rcy[k] = sl.rvr[(4 + k) * EPB + el]; }
+        uint32_t f = quads_intersect(rcx, rcy, hcx, hcy) ? LF_VR : 0u;
+        if (!(np_norm2(px - HF(sl, H_GX, tid), py - HF(sl, H_GY, tid)) < rad)) f |= LF_NOTREACHED;
+        sl.lf[tid] = f;
+    }
+    __syncthreads();
+
+    // ---- phase 3: calc_reward ladder + robot kinematics + Monitor (env lanes) ---------------------
+    if (rl) {
+        const double rpx = RF(sl, R_PX, tid, EPB), rpy = RF(sl, R_PY, tid, EPB), rr = RF(sl, R_RAD, tid, EPB);
+        const double rgx = RF(sl, R_GX, tid, EPB), rgy = RF(sl, R_GY, tid, EPB);
+        const uint32_t flags = sl.rflag[tid];
+        const bool rf32 = (flags & CN_FLAG_ROBOT_F32) != 0;
+        const float a0 = sl.act[tid], a1 = sl.act[EPB + tid];
+        const int eb = tid * N;
+        double dmin = INFINITY;
+        bool collision = false, nz_viol = false, nz_checked = false;
+        int vr_viol = 0, agg = 0;
+        for (int k = 0; k < N; ++k) {
+            const double cd = sl.cd[eb + k];
+            if (cd < 0) { collision = true; break; }
+            else if (cd < dmin) dmin = cd;
+            if (c.norm_zones && !nz_checked) {
+                nz_checked = true;
+                double zx[4], zy[4];
+                for (int z = 0; z < 2 && !nz_viol; ++z) {
+                    norm_zone(rpx, rpy, RF(sl, R_VX, tid, EPB), RF(sl, R_VY, tid, EPB), rr, rf32, c.norm_zone_lhs,
+                              z == 0, zx, zy);
+                    if (disc_quad_intersect(rpx, rpy, rr, zx, zy)) nz_viol = true;
+                }
+            }
+            const uint32_t f = sl.lf[eb + k];
+            vr_viol += (f & LF_VR) ? 1 : 0;
+            agg += (f & LF_NOTREACHED) ? 1 : 0;
+        }
+        const bool reaching_goal = np_norm2(rpx - rgx, rpy - rgy) < rr;
+        if (!reaching_goal) ++agg;
+        // commanded world-frame velocity; unicycle: theta + r is float32 (NEP 50)
+        const float tr = (float)RF(sl, R_TH, tid, EPB) + a1;
+        const float th_new = np_modf(tr, (float)(2 * CN_PI));
+        double cvx, cvy;
+        if (holo) { cvx = a0; cvy = a1; }
+        else { cvx = (double)(a0 * np_cosf(th_new)); cvy = (double)(a0 * np_sinf(th_new)); }
+        // unicycle differential drive (agent.py:185-194)
+        double upx = rpx, upy = rpy;
+        if (!holo && !(fabsf(a1) < 0.0001f)) {
+            const float w = fdiv(a1, (float)dt);
+            const float R = fdiv(a0, w);
+            const double th = RF(sl, R_TH, tid, EPB);
+            double t1x, t1y;
+            if (rf32) { t1x = (double)(R * np_sinf((float)th)); t1y = (double)(R * np_cosf((float)th)); }
+            else { t1x = (double)R * sin(th); t1y = (double)R * cos(th); }
+            upx = rpx - t1x + (double)(R * np_sinf(tr));
+            upy = rpy + t1y - (double)(R * np_cosf(tr));
+        }
+        double side_l = 0, side_r = 0, sep = 0;
+        if (c.side_preference) {
+            double ex, ey;
+            if (holo) { ex = rpx + (double)(a0 * (float)dt); ey = rpy + (double)(a1 * (float)dt); }
+            else { ex = upx; ey = upy; }
+            const double hy = HF(sl, H_PY, eb), hr = HF(sl, H_R, eb);
+            if (ey <= hy + hr && ey >= hy - hr) { if (ex < HF(sl, H_PX, eb)) side_l = 1; else side_r = 1; }
+            sep = np_norm2(HF(sl, H_PX, eb) - rpx, HF(sl, H_PY, eb) - rpy);
+        }
+        double jerk;
+        {
+            const float ax = (float)cvx - (float)RF(sl, R_VX, tid, EPB), ay = (float)cvy - (float)RF(sl, R_VY, tid, EPB);
+            const float dax = ax - (float)S.last_ax[ge], day = ay - (float)S.last_ay[ge];
+            jerk = (double)(dax * dax + day * day);
+            S.last_ax[ge] = ax; S.last_ay[ge] = ay;
+        }
+        const double dist_to_goal = np_norm2(rpx - rgx, rpy - rgy);
+        const bool inside = inside_world(rpx, rpy, rr, c.square_width / 2);
+        double speed;
+        { const float fx = (float)cvx, fy = (float)cvy; speed = (double)fsqrt(fx * fx + fy * fy); }
+        const double gt = RF(sl, R_GT, tid, EPB);
+        double reward;
+        int done, event;
+        if (gt >= c.time_limit - 1) { reward = 0; done = 1; event = CN_EV_TIMEOUT; }
+        else if (collision || !inside) { reward = c.collision_penalty; done = 1; event = CN_EV_COLLISION; }
+        else if (reaching_goal) {
+            reward = c.success_reward;
+            if (c.time_factor) reward *= ddiv(c.time_limit - gt, c.time_limit);
+            done = 1; event = CN_EV_REACHGOAL;
+        } else if (dmin < c.discomfort_dist) {
+            reward = (dmin - c.discomfort_dist) * c.discomfort_penalty_factor;
+            done = 0; event = CN_EV_DANGER;
+        } else {
+            reward = c.potential_factor * (-fabs(dist_to_goal) - RF(sl, R_POT, tid, EPB));
+            RF(sl, R_POT, tid, EPB) = -fabs(dist_to_goal);
+            if (c.norm_zones && nz_viol) reward += c.norm_zone_penalty;
+            done = 0; event = CN_EV_NOTHING;
+        }
+        if (!holo) {
+            const float r_spin = -2.0f * (a1 * a1);
+            const float r_back = a0 < 0 ? -2.0f * fabsf(a0) : 0.0f;
+            if (event == CN_EV_DANGER || event == CN_EV_NOTHING) reward = reward + (double)r_spin + (double)r_back;
+            else reward = (double)(((float)reward + r_spin) + r_back);
+        }
+        if (g.info) {
+            float *info = g.info + ge * CN_INFO_K;
+            info[CN_INFO_AGG_NAV_TIME] = (float)agg;
+            info[CN_INFO_PATH_VIOLATION] = (float)vr_viol;
+            info[CN_INFO_PERSONAL_VIOLATION] = dmin < c.min_personal_space ? 1.0f : 0.0f;
+            info[CN_INFO_JERK_COST] = (float)jerk;
+            info[CN_INFO_DIST_TO_GOAL] = (float)dist_to_goal;
+            info[CN_INFO_SPEED_VIOLATION] = speed > c.max_walking_speed ? 1.0f : 0.0f;
+            info[CN_INFO_MIN_DIST] = (float)dmin;
+            info[CN_INFO_SCENARIO] = (float)S.scenario[ge];
+            info[CN_INFO_SIDE_LEFT] = (float)side_l;
+            info[CN_INFO_SIDE_RIGHT] = (float)side_r;
+            info[CN_INFO_SEPARATION] = (float)sep;
+            info[CN_INFO_OVERFLOW] = (float)S.overflow[ge];
+        }
+        // robot kinematics (agent.py:198-212)
+        if (holo) {
+            RF(sl, R_NX, tid, EPB) = rpx + (double)(a0 * (float)dt);
+            RF(sl, R_NY, tid, EPB) = rpy + (double)(a1 * (float)dt);
+            RF(sl, R_VX, tid, EPB) = a0; RF(sl, R_VY, tid, EPB) = a1;
+        } else {
+            RF(sl, R_NX, tid, EPB) = upx; RF(sl, R_NY, tid, EPB) = upy;
+            RF(sl, R_TH, tid, EPB) = th_new;
+            RF(sl, R_VX, tid, EPB) = cvx; RF(sl, R_VY, tid, EPB) = cvy;
+        }
+        sl.rflag[tid] = flags | CN_FLAG_ROBOT_F32;
+        RF(sl, R_GT, tid, EPB) = gt + dt;
+        const double epr = S.ep_return[ge] + reward;
+        const int32_t epl = S.ep_len[ge] + 1;
+        S.ep_return[ge] = epr; S.ep_len[ge] = epl;
+        if (g.reward) g.reward[ge] = (float)reward;
+        if (g.done) g.done[ge] = (uint8_t)done;
+        if (g.event) g.event[ge] = (int8_t)event;
+        if (g.ep_return) g.ep_return[ge] = epr;
+        if (g.ep_len) g.ep_len[ge] = epl;
+        sl.rflag[EPB + tid] = (uint32_t)done;   // aux word: done
+    }
+    __syncthreads();
+
+    // ---- phase 4: human kinematics, observation, goal-change detection ---------------------------
+    if (hl) {
+        const double npx = HF(sl, H_PX, tid) + nvx * dt, npy = HF(sl, H_PY, tid) + nvy * dt;
+        S.h_px[gh] = npx; S.h_py[gh] = npy; S.h_vx[gh] = nvx; S.h_vy[gh] = nvy;
+        // detect_visible(robot, human, robot1=True) on the POST-move state (robot velocity now float32)
+        double fx, fy;
+        if (holo) fov_dir32(atan2f((float)RF(sl, R_VY, el, EPB), (float)RF(sl, R_VX, el, EPB)), fx, fy);
+        else fov_dir32((float)RF(sl, R_TH, el, EPB), fx, fy);
+        const double rnx = RF(sl, R_NX, el, EPB), rny = RF(sl, R_NY, el, EPB);
+        if (in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov)) {
+            bpx = npx; bpy = npy; bvx = nvx; bvy = nvy; br = HF(sl, H_R, tid);
+        } else {
+            bpx = bpx + bvx * dt; bpy = bpy + bvy * dt;
+        }
+        S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = bvx; S.b_vy[gh] = bvy; S.b_r[gh] = br;
+        g.spatial[gh * 2] = (float)(bpx - rnx);
+        g.spatial[gh * 2 + 1] = (float)(bpy - rny);
+        uint32_t f = sl.lf[tid] & ~LF_ENDGOAL;
+        if (np_norm2(HF(sl, H_GX, tid) - npx, HF(sl, H_GY, tid) - npy) < HF(sl, H_R, tid)) f |= LF_ENDGOAL;
+        if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
+        sl.lf[tid] = f;
+    }
+    __syncthreads();
+    if (rl) {
+        const double nx = RF(sl, R_NX, tid, EPB), ny = RF(sl, R_NY, tid, EPB);
+        S.r_px[ge] = nx; S.r_py[ge] = ny;
+        S.r_vx[ge] = RF(sl, R_VX, tid, EPB); S.r_vy[ge] = RF(sl, R_VY, tid, EPB);
+        S.r_theta[ge] = RF(sl, R_TH, tid, EPB);
+        S.r_dv[ge] = RF(sl, R_DV, tid, EPB);
+        S.potential[ge] = RF(sl, R_POT, tid, EPB);
+        const double gt = RF(sl, R_GT, tid, EPB);
+        S.gtime[ge] = gt;
+        uint32_t flags = sl.rflag[tid];
+        if (orca) flags |= CN_FLAG_ORCA_FROZEN;
+        bool endg = false, nan = false;
+        for (int k = 0; k < N; ++k) {
+            const uint32_t f = sl.lf[tid * N + k];
+            endg |= (f & LF_ENDGOAL) != 0;
+            nan |= (f & 0x80000000u) != 0;
+        }
+        if (nan) flags |= CN_FLAG_NAN;
+        S.flags[ge] = flags;
+        float *rn = g.robot_node + ge * 7;
+        rn[0] = (float)nx; rn[1] = (float)ny; rn[2] = (float)RF(sl, R_RAD, tid, EPB);
+        rn[3] = (float)RF(sl, R_GX, tid, EPB); rn[4] = (float)RF(sl, R_GY, tid, EPB);
+        rn[5] = (float)RF(sl, R_VP, tid, EPB); rn[6] = (float)RF(sl, R_TH, tid, EPB);
+        g.temporal[ge * 2] = (float)RF(sl, R_VX, tid, EPB);
+        g.temporal[ge * 2 + 1] = (float)RF(sl, R_VY, tid, EPB);
+        // random numbers needed? (crowd_sim_dict.py:260-269, shmem_vec_env.py:166-167)
+        const bool done = sl.rflag[EPB + tid] != 0;
+        const bool rgoal = c.random_goal_changing && np_mod(gt, 5.0) == 0.0;
+        const bool egoal = c.end_goal_changing && endg;
+        if (done || rgoal || egoal) {
+            const uint32_t slot = atomicAdd(g.work_count, 1u);
+            g.work[slot] = (uint32_t)ge | (done ? 0x80000000u : 0u);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// kernel B: RNG work (goal changes, auto-reset) — one 64-lane workgroup per listed env
+// ------------------------------------------------------------------------------------------------
+struct RngArgs {
+    cn_state_ptrs s;
+    const uint32_t *work;
+    const uint32_t *work_count;
+    int reset_all;          // cn_reset: every env, done = 1
+    int E;
+    int64_t case_size, counter_offset;
+    float *robot_node, *temporal, *spatial;
+};
+
+struct MT {
+    uint32_t *w;  // LDS [624]
+    int pos;
+    bool twisted;
+    __device__ uint32_t next()
+    {
+        if (pos >= CN_MT_N) {  // mt19937_gen, sequential (rare: once per 312 doubles)
+            int k;
+            for (k = 0; k < CN_MT_N - 397; ++k) w[k] = mt_mix(w[k], w[k + 1], w[k + 397]);
+            for (; k < CN_MT_N - 1; ++k) w[k] = mt_mix(w[k], w[k + 1], w[k + (397 - CN_MT_N)]);
+            w[CN_MT_N - 1] = mt_mix(w[CN_MT_N - 1], w[0], w[396]);
+            pos = 0;
+            twisted = true;
+        }
+        return mt_temper(w[pos++]);
+    }
+    __device__ double rnd()
+    {
+        const int32_t a = (int32_t)(next() >> 5), b = (int32_t)(next() >> 6);
+        return (a * 67108864.0 + b) / 9007199254740992.0;
+    }
+    __device__ double unif(double lo, double hi) { return lo + (hi - lo) * rnd(); }
+};
+
+// wave-cooperative mt19937_gen on LDS words (64 lanes)
+__device__ inline void mt_twist_wave(uint32_t *w, int lane)
+{
+    uint32_t nv[4];
+    // part 1: k in [0, 227): reads old words only
+    for (int r = 0; r < 4; ++r) {
+        const int k = lane + 64 * r;
+        if (k < CN_MT_N - 397) nv[r] = mt_mix(w[k], w[k + 1], w[k + 397]);
+    }
+    __syncthreads();
+    for (int r = 0; r < 4; ++r) { const int k = lane + 64 * r; if (k < CN_MT_N - 397) w[k] = nv[r]; }
+    __syncthreads();
+    // part 2: k in [227, 623): w[k - 227] is new (part 1), w[k], w[k+1] old -> chunks of 227
+    for (int base = CN_MT_N - 397; base < CN_MT_N - 1; base += 227) {
+        const int end = min(base + 227, CN_MT_N - 1);
+        uint32_t v[4];
+        for (int r = 0; r < 4; ++r) {
+            const int k = base + lane + 64 * r;
+            if (k < end) v[r] = mt_mix(w[k], w[k + 1], w[k + (397 - CN_MT_N)]);
+        }
+        __syncthreads();
+        for (int r = 0; r < 4; ++r) { const int k = base + lane + 64 * r; if (k < end) w[k] = v[r]; }
+        __syncthreads();
+    }
+    if (lane == 0) w[CN_MT_N - 1] = mt_mix(w[CN_MT_N - 1], w[0], w[396]);
+    __syncthreads();
+}
+
+struct Env1 {  // one env's agents in LDS (kernel B)
+    double rpx, rpy, rgx, rgy, rr;
+    double *hpx, *hpy, *hgx, *hgy, *hr, *hvp, *hth;  // [N]
+};
+
+__device__ inline double rand_world_pt(const cn_config &c, MT &m) { return (m.rnd() - 0.5) * c.square_width / 2; }
+
+__device__ void create_agent_attributes(const cn_config &c, MT &m, int scenario, double agent_vpref, double agent_radius,
+                                        double robot_radius, double &px, double &py, double &gx, double &gy,
+                                        double &heading, double &vp)
+{
+    double v_pref = agent_vpref == 0 ? 1.0 : agent_vpref;
+    const double pxn = (m.rnd() - 0.5) * v_pref;
+    const double pyn = (m.rnd() - 0.5) * v_pref;
+    const double R = c.circle_radius;
+    heading = 0;
+    switch (scenario) {
+    case CN_SC_CIRCLE_CROSSING: {
+        const double angle = m.rnd() * CN_PI * 2;
+        px = R * cos(angle) + pxn; py = R * sin(angle) + pyn;
+        gx = -px; gy = -py;
+    } break;
+    case CN_SC_SQUARE_CROSSING:
+        px = rand_world_pt(c, m) * 0.4 + pxn;
+        py = rand_world_pt(c, m) * 0.4 + pyn;
+        gx = rand_world_pt(c, m) * 0.4 + pxn;
+        gy = rand_world_pt(c, m) * 0.4 + pyn;
+        break;
+    case CN_SC_PARALLEL_TRAFFIC: {
+        const double sign = m.rnd() >= 0.5 ? 1 : -1;
+        px = rand_world_pt(c, m) * 0.4 + pxn;
+        py = sign * (m.rnd() * 3 + 1 + pyn);
+        gx = px; gy = -py;
+    } break;
+    case CN_SC_PERPENDICULAR_TRAFFIC: {
+        const double sign = m.rnd() >= 0.5 ? 1 : -1;
+        px = sign * (m.rnd() * 3 + 1 + pxn);
+        gx = -px;
+        py = rand_world_pt(c, m) * 0.4 + pyn;
+        gy = py;
+    } break;
+    case CN_SC_SIDE_PREF_PASSING:
+    case CN_SC_SIDE_PREF_OVERTAKING: {
+        const double min_x = -(robot_radius + agent_radius), max_x = -min_x;
+        const double hx = (max_x - min_x) * m.rnd() + min_x;
+        px = hx; gx = hx;
+        if (scenario == CN_SC_SIDE_PREF_PASSING) { py = R; gy = -R; heading = -CN_PI / 2; }
+        else { py = -R + 2; gy = R + 2; heading = CN_PI / 2; v_pref = 0.3; }
+    } break;
+    default: {
+        const double min_x = -(R + robot_radius + agent_radius), max_x = -(R - robot_radius - agent_radius);
+        const double hx = (max_x - min_x) * m.rnd() + min_x;
+        px = hx; gx = -hx; py = 0; gy = 0;
+    } break;
+    }
+    vp = v_pref;
+}
+
+// goal candidate rejection test against the robot and all other humans (positions AND goals)
+__device__ inline bool goal_collides(const cn_config &c, const Env1 &en, int N, int self, double gx, double gy)
+{
+    for (int a = -1; a < N; ++a) {
+        if (a == self) continue;
+        double ax, ay, agx, agy, ar;
+        if (a < 0) { ax = en.rpx; ay = en.rpy; agx = en.rgx; agy = en.rgy; ar = en.rr; }
+        else { ax = en.hpx[a]; ay = en.hpy[a]; agx = en.hgx[a]; agy = en.hgy[a]; ar = en.hr[a]; }
+        const double md = en.hr[self] + ar + c.discomfort_dist;
+        if (np_norm2(gx - ax, gy - ay) < md || np_norm2(gx - agx, gy - agy) < md) return true;
+    }
+    return false;
+}
+
+__global__ void __launch_bounds__(64) cn_rng_kernel(RngArgs g, cn_config c)
+{
+    __shared__ uint32_t mtw[CN_MT_N];
+    __shared__ double hbuf[7][32];
+    __shared__ double rbuf[8];
+    __shared__ uint32_t misc[4];
+    const cn_state_ptrs &S = g.s;
+    const int lane = threadIdx.x;
+    const int N = c.human_num;
+    const uint32_t nwork = g.reset_all ? (uint32_t)g.E : *g.work_count;
+    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+        const uint32_t item = g.reset_all ? (w | 0x80000000u) : g.work[w];
+        const int64_t e = item & 0x7fffffffu;
+        const bool done = (item >> 31) != 0;
+        Env1 en;
+        en.hpx = hbuf[0]; en.hpy = hbuf[1]; en.hgx = hbuf[2]; en.hgy = hbuf[3]; en.hr = hbuf[4]; en.hvp = hbuf[5];
+        en.hth = hbuf[6];
+        const int64_t hb = e * N;
+        if (!done) {
+            // ---------------- goal changes (crowd_sim_dict.py:260-269) ----------------
+            for (int k = lane; k < CN_MT_N; k += 64) mtw[k] = S.mt[e * CN_MT_N + k];
+            if (lane < N) {
+                en.hpx[lane] = S.h_px[hb + lane]; en.hpy[lane] = S.h_py[hb + lane];
+                en.hgx[lane] = S.h_gx[hb + lane]; en.hgy[lane] = S.h_gy[hb + lane];
+                en.hr[lane] = S.h_r[hb + lane]; en.hvp[lane] = S.h_vpref[hb + lane];
+            }
+            __syncthreads();
+            if (lane == 0) {
+                en.rpx = S.r_px[e]; en.rpy = S.r_py[e]; en.rgx = S.r_gx[e]; en.rgy = S.r_gy[e]; en.rr = S.r_radius[e];
+                MT m{mtw, S.mt_pos[e], false};
+                uint32_t ovf = S.overflow[e];
+                const int sc = S.scenario[e];
+                if (c.random_goal_changing && np_mod(S.gtime[e], 5.0) == 0.0) {
+                    // update_human_goals_randomly (crowd_sim.py:724-766)
+                    for (int i = 0; i < N; ++i) {
+                        if (en.hvp[i] == 0) continue;
+                        if (m.rnd() <= c.goal_change_chance) {
+                            double gx = 0, gy = 0;
+                            for (int t = 0;; ++t) {
+                                const double angle = m.rnd() * CN_PI * 2;
+                                const double vp = en.hvp[i] == 0 ? 1.0 : en.hvp[i];
+                                const double gxn = (m.rnd() - 0.5) * vp, gyn = (m.rnd() - 0.5) * vp;
+                                gx = c.circle_radius * cos(angle) + gxn;
+                                gy = c.circle_radius * sin(angle) + gyn;
+                                if (!goal_collides(c, en, N, i, gx, gy)) break;
+                                if (t + 1 >= c.max_tries) { ++ovf; break; }
+                            }
+                            en.hgx[i] = gx; en.hgy[i] = gy;
+                        }
+                    }
+                }
+                if (c.end_goal_changing) {
+                    // update_human_goal (crowd_sim.py:769-811) for humans within radius of their goal
+                    for (int i = 0; i < N; ++i) {
+                        if (!(np_norm2(en.hgx[i] - en.hpx[i], en.hgy[i] - en.hpy[i]) < en.hr[i])) continue;
+                        if (m.rnd() <= c.end_goal_change_chance) {
+                            if (c.random_radii) en.hr[i] += m.unif(-0.1, 0.1);
+                            if (c.random_v_pref) en.hvp[i] += m.unif(-0.1, 0.1);
+                            double gx = 0, gy = 0;
+                            for (int t = 0;; ++t) {
+                                double px, py, hd, vp;
+                                create_agent_attributes(c, m, sc, en.hvp[i], en.hr[i], en.rr, px, py, gx, gy, hd, vp);
+                                if (!goal_collides(c, en, N, i, gx, gy)) break;
+                                if (t + 1 >= c.max_tries) { ++ovf; break; }
+                            }
+                            en.hgx[i] = gx; en.hgy[i] = gy;
+                        }
+                    }
+                }
+                S.mt_pos[e] = m.pos;
+                S.overflow[e] = ovf;
+                misc[0] = m.twisted ? 1u : 0u;
+            }
+            __syncthreads();
+            if (lane < N) {
+                S.h_gx[hb + lane] = en.hgx[lane]; S.h_gy[hb + lane] = en.hgy[lane];
+                S.h_r[hb + lane] = en.hr[lane]; S.h_vpref[hb + lane] = en.hvp[lane];
+            }
+            if (misc[0]) for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[k];
+            __syncthreads();
+            continue;
+        }
+        // ---------------- CrowdSimDict.reset (crowd_sim_dict.py:105-203) ----------------
+        const int64_t gidx = c.env_offset + e;
+        if (lane == 0) {
+            int sc;
+            if (c.scenario_mode == CN_SCMODE_SEQUENTIAL) sc = c.scenarios[S.reset_count[e] % c.num_scenarios];
+            else sc = c.scenarios[gidx % c.num_scenarios];
+            misc[1] = (uint32_t)sc;
+            uint32_t seed = (uint32_t)(g.counter_offset + S.case_counter[e] + (c.seed + gidx));
+            for (int k = 0; k < CN_MT_N; ++k) {  // mt19937_seed: sequential Knuth chain
+                mtw[k] = seed;
+                seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(k + 1);
+            }
+        }
+        __syncthreads();
+        mt_twist_wave(mtw, lane);
+        if (lane == 0) {
+            MT m{mtw, 0, false};
+            const int sc = (int)misc[1];
+            uint32_t ovf = 0;
+            const double R = c.circle_radius;
+            en.rr = c.robot_radius;
+            double rth;
+            if (c.kinematics == CN_UNICYCLE) {
+                const double angle = m.unif(0, CN_PI * 2);
+                en.rpx = R * cos(angle); en.rpy = R * sin(angle);
+                for (int t = 0;; ++t) {
+                    en.rgx = m.unif(-R, R); en.rgy = m.unif(-R, R);
+                    if (np_norm2(en.rpx - en.rgx, en.rpy - en.rgy) >= 6) break;
+                    if (t + 1 >= c.max_tries) { ++ovf; break; }
+                }
+                rth = m.unif(0, 2 * CN_PI);
+            } else if (c.social_metrics || c.side_preference) {
+                en.rpx = 0; en.rpy = -R; en.rgx = 0; en.rgy = R; rth = CN_PI / 2;
+            } else {
+                for (int t = 0;; ++t) {
+                    en.rpx = m.unif(-R, R); en.rpy = m.unif(-R, R); en.rgx = m.unif(-R, R); en.rgy = m.unif(-R, R);
+                    if (np_norm2(en.rpx - en.rgx, en.rpy - en.rgy) >= 6) break;
+                    if (t + 1 >= c.max_tries) { ++ovf; break; }
+                }
+                rth = CN_PI / 2;
+            }
+            for (int i = 0; i < N; ++i) {
+                double vpref = c.human_vpref, rad = c.human_radius;
+                if (c.randomize_attributes) { vpref = m.unif(0.5, 1.5); rad = m.unif(0.3, 0.5); }
+                double px = 0, py = 0, gx = 0, gy = 0, hd = 0, vp = 0;
+                for (int t = 0;; ++t) {
+                    create_agent_attributes(c, m, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
+                    bool collide = false;
+                    for (int a = 0; a <= i; ++a) {
+                        double md, ax, ay;
+                        if (a == 0) {
+                            ax = en.rpx; ay = en.rpy;
+                            md = c.kinematics == CN_UNICYCLE ? R / 2 : rad + en.rr + c.discomfort_dist;
+                        } else {
+                            ax = en.hpx[a - 1]; ay = en.hpy[a - 1];
+                            md = rad + en.hr[a - 1] + c.discomfort_dist;
+                        }
+                        if (np_norm2(px - ax, py - ay) < md) { collide = true; break; }
+                    }
+                    if (!collide) break;
+                    if (t + 1 >= c.max_tries) { ++ovf; break; }
+                }
+                en.hpx[i] = px; en.hpy[i] = py; en.hgx[i] = gx; en.hgy[i] = gy;
+                en.hth[i] = hd; en.hvp[i] = vp; en.hr[i] = rad;
+            }
+            rbuf[0] = en.rpx; rbuf[1] = en.rpy; rbuf[2] = en.rgx; rbuf[3] = en.rgy; rbuf[4] = rth;
+            misc[0] = ovf;
+            misc[2] = (uint32_t)m.pos;
+        }
+        __syncthreads();
+        const double rpx = rbuf[0], rpy = rbuf[1];
+        if (lane < N) {
+            const int64_t h = hb + lane;
+            const double px = en.hpx[lane], py = en.hpy[lane];
+            S.h_px[h] = px; S.h_py[h] = py; S.h_gx[h] = en.hgx[lane]; S.h_gy[h] = en.hgy[lane];
+            S.h_vx[h] = 0.0; S.h_vy[h] = 0.0; S.h_r[h] = en.hr[lane]; S.h_vpref[h] = en.hvp[lane];
+            S.h_theta[h] = en.hth[lane];
+            S.o_r[h] = 0.0f; S.o_vmax[h] = 0.0f; S.o_dmask[h] = 0u;
+            // generate_ob(reset=True): robot velocity is 0 (ints) -> float64 FOV path
+            double fx, fy;
+            if (c.kinematics == CN_HOLONOMIC) fov_dir64(atan2(0.0, 0.0), fx, fy);
+            else fov_dir64(rbuf[4], fx, fy);
+            double bpx, bpy, bvx, bvy, br;
+            if (in_fov(fx, fy, rpx, rpy, px, py, c.robot_fov)) { bpx = px; bpy = py; bvx = 0; bvy = 0; br = en.hr[lane]; }
+            else { bpx = 15.0; bpy = 15.0; bvx = 0.0; bvy = 0.0; br = 0.3; }
+            S.b_px[h] = bpx; S.b_py[h] = bpy; S.b_vx[h] = bvx; S.b_vy[h] = bvy; S.b_r[h] = br;
+            g.spatial[h * 2] = (float)(bpx - rpx);
+            g.spatial[h * 2 + 1] = (float)(bpy - rpy);
+        }
+        const int A = N + (c.robot_visible ? 1 : 0);
+        if (A > 10) for (int k = lane; k < N * A; k += 64) S.o_perm[e * N * A + k] = 0;
+        for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[k];
+        if (lane == 0) {
+            S.scenario[e] = (int32_t)misc[1];
+            S.gtime[e] = 0.0; S.r_dv[e] = 0.0;
+            S.r_px[e] = rpx; S.r_py[e] = rpy; S.r_gx[e] = rbuf[2]; S.r_gy[e] = rbuf[3]; S.r_theta[e] = rbuf[4];
+            S.r_vx[e] = 0.0; S.r_vy[e] = 0.0; S.r_radius[e] = c.robot_radius; S.r_vpref[e] = c.robot_vpref;
+            S.case_counter[e] = (S.case_counter[e] + c.nenv) % g.case_size;
+            S.potential[e] = -fabs(np_norm2(rpx - rbuf[2], rpy - rbuf[3]));
+            S.reset_count[e] += 1;
+            S.ep_return[e] = 0.0; S.ep_len[e] = 0;
+            S.flags[e] = 0; S.overflow[e] = misc[0]; S.mt_pos[e] = (int32_t)misc[2];
+            float *rn = g.robot_node + e * 7;
+            rn[0] = (float)rpx; rn[1] = (float)rpy; rn[2] = (float)c.robot_radius;
+            rn[3] = (float)rbuf[2]; rn[4] = (float)rbuf[3]; rn[5] = (float)c.robot_vpref; rn[6] = (float)rbuf[4];
+            g.temporal[e * 2] = 0.0f; g.temporal[e * 2 + 1] = 0.0f;
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fused DSRNN edge-feature assembly (srnn_model.py:160-161, 210-211, 466)
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) cn_edge_features_kernel(int64_t E, int N, const float *__restrict__ robot_node,
+                                                               const float *__restrict__ temporal,
+                                                               const float *__restrict__ spatial,
+                                                               const float *__restrict__ Wt, const float *__restrict__ bt,
+                                                               const float *__restrict__ Ws, const float *__restrict__ bs,
+                                                               const float *__restrict__ Wr, const float *__restrict__ br,
+                                                               const float *__restrict__ Wn, const float *__restrict__ bn,
+                                                               float *__restrict__ t_out, float *__restrict__ s_out,
+                                                               float *__restrict__ n_out)
+{
+    // one thread per (row, 4 output features); rows = E temporal + E*N spatial + E node
+    const int64_t rows = E * (N + 2);
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t row = idx >> 4;
+    const int q = (int)(idx & 15) * 4;
+    if (row >= rows) return;
+    float o[4];
+    if (row < E) {  // temporal edge: relu(Wt x + bt), x = robot velocity
+        const float x0 = temporal[row * 2], x1 = temporal[row * 2 + 1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = fmaxf(__fmaf_rn(Wt[(q + k) * 2 + 1], x1, __fmaf_rn(Wt[(q + k) * 2], x0, bt[q + k])), 0.0f);
+        *(float4 *)(t_out + row * 64 + q) = make_float4(o[0], o[1], o[2], o[3]);
+    } else if (row < E + E * N) {  // spatial edges
+        const int64_t r = row - E;
+        const float x0 = spatial[r * 2], x1 = spatial[r * 2 + 1];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = fmaxf(__fmaf_rn(Ws[(q + k) * 2 + 1], x1, __fmaf_rn(Ws[(q + k) * 2], x0, bs[q + k])), 0.0f);
+        *(float4 *)(s_out + r * 64 + q) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {  // robot node: relu(Wn (Wr x + br) + bn)
+        const int64_t r = row - E - E * N;
+        float h[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            float a = br[j];
+#pragma unroll
+            for (int k = 0; k < 7; ++k) a = __fmaf_rn(Wr[j * 7 + k], robot_node[r * 7 + k], a);
+            h[j] = a;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float a = bn[q + k];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) a = __fmaf_rn(Wn[(q + k) * 3 + j], h[j], a);
+            o[k] = fmaxf(a, 0.0f);
+        }
+        *(float4 *)(n_out + r * 64 + q) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
+struct cn_engine {
+    cn_config c;
+    int device;
+    int E, N, A;
+    StepPlan plan;
+    void *state;
+    int64_t state_bytes;
+    cn_state_ptrs s;
+    uint32_t *work;       // [E]
+    uint32_t *work_count; // [4]
+    int64_t case_size, counter_offset;
+    int rng_grid;
+};
+
+static thread_local char g_err[512];
+static int set_err(int code, const char *fmt, const char *a = "")
+{
+    snprintf(g_err, sizeof g_err, fmt, a);
+    return code;
+}
+#define HIPCHK(x)                                                                       \
+    do {                                                                                \
+        hipError_t _e = (x);                                                            \
+        if (_e != hipSuccess) return set_err(CN_EHIP, "HIP error: %s", hipGetErrorString(_e)); \
+    } while (0)
+
+extern "C" {
+
+const char *cn_last_error(void) { return g_err; }
+const char *cn_version(void) { return "crowdnav_dsrnn_amd 0.1 (gfx950)"; }
+
+int cn_config_validate(const cn_config *c)
+{
+    if (!c) return set_err(CN_EINVAL, "null config");
+    if (c->num_envs <= 0) return set_err(CN_EINVAL, "num_envs must be > 0");
+    if (c->human_num < 1 || c->human_num > 31) return set_err(CN_EUNSUPPORTED, "human_num must be in [1, 31]");
+    if (c->human_num + (c->robot_visible ? 1 : 0) > CN_MAX_A) return set_err(CN_EUNSUPPORTED, "too many agents");
+    if (c->num_scenarios < 1 || c->num_scenarios > CN_MAX_SCENARIOS) return set_err(CN_EINVAL, "num_scenarios");
+    for (int k = 0; k < c->num_scenarios; ++k)
+        if (c->scenarios[k] < 0 || c->scenarios[k] > CN_SC_SIDE_PREF_CROSSING) return set_err(CN_EINVAL, "scenario id");
+    if (c->kinematics != CN_HOLONOMIC && c->kinematics != CN_UNICYCLE) return set_err(CN_EINVAL, "kinematics");
+    if (c->human_policy != CN_POLICY_ORCA && c->human_policy != CN_POLICY_SOCIAL_FORCE)
+        return set_err(CN_EUNSUPPORTED, "human policy");
+    if (!c->potential_based) return set_err(CN_EUNSUPPORTED, "only potential-based reward shaping is supported");
+    if (!(c->time_step > 0)) return set_err(CN_EINVAL, "time_step must be > 0");
+    if (c->phase < 0 || c->phase > 2) return set_err(CN_EINVAL, "phase");
+    if (c->nenv <= 0) return set_err(CN_EINVAL, "nenv must be > 0");
+    if (c->max_tries <= 0) return set_err(CN_EINVAL, "max_tries must be > 0");
+    return CN_OK;
+}
+
+int cn_state_field_info(int field, const char **name, int *type_code, int *count_kind)
+{
+    static const char *names[] = {
+#define X(n, ct, tc, ck) #n,
+        CN_STATE_FIELDS(X)
+#undef X
+    };
+    static const int tcs[] = {
+#define X(n, ct, tc, ck) tc,
+        CN_STATE_FIELDS(X)
+#undef X
+    };
+    static const int cks[] = {
+#define X(n, ct, tc, ck) ck,
+        CN_STATE_FIELDS(X)
+#undef X
+    };
+    if (field < 0 || field >= CN_NUM_FIELDS) return set_err(CN_EINVAL, "field index");
+    if (name) *name = names[field];
+    if (type_code) *type_code = tcs[field];
+    if (count_kind) *count_kind = cks[field];
+    return CN_OK;
+}
+
+int cn_state_layout_offsets(const cn_config *cfg, int64_t *offsets, int64_t *total)
+{
+    if (!cfg) return set_err(CN_EINVAL, "null config");
+    const int64_t t = cn_state_layout(cfg->num_envs, cfg->human_num, cfg->robot_visible, offsets);
+    if (total) *total = t;
+    return CN_OK;
+}
+
+int cn_create(const cn_config *cfg, int device, cn_engine **out)
+{
+    if (!out) return set_err(CN_EINVAL, "null out");
+    *out = nullptr;
+    int rc = cn_config_validate(cfg);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(device));
+    cn_engine *g = new cn_engine();
+    g->c = *cfg;
+    g->device = device;
+    g->E = cfg->num_envs;
+    g->N = cfg->human_num;
+    g->A = cn_sim_agents(g->N, cfg->robot_visible);
+    g->plan = cn_step_plan(g->N, cfg->robot_visible);
+    g->state_bytes = cn_state_layout(g->E, g->N, cfg->robot_visible, nullptr);
+    switch (cfg->phase) {
+    case CN_PHASE_TRAIN: g->case_size = 4294967295LL - 2000; g->counter_offset = 2000; break;
+    case CN_PHASE_VAL: g->case_size = cfg->val_size; g->counter_offset = 0; break;
+    default: g->case_size = cfg->test_size; g->counter_offset = 1000; break;
+    }
+    if (g->case_size <= 0) { delete g; return set_err(CN_EINVAL, "case size (val_size/test_size) must be > 0"); }
+    hipError_t e1 = hipMalloc(&g->state, g->state_bytes);
+    hipError_t e2 = hipMalloc(&g->work, sizeof(uint32_t) * (g->E + 64));
+    hipError_t e3 = hipMalloc(&g->work_count, 64);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+        hipFree(g->state); hipFree(g->work); hipFree(g->work_count);
+        delete g;
+        return set_err(CN_ENOMEM, "hipMalloc failed");
+    }
+    hipMemset(g->state, 0, g->state_bytes);
+    hipMemset(g->work_count, 0, 64);
+    cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
+    // unit-circle table of GEOS's 64-gon point buffer (norm zones)
+    double cs[64], sn[64];
+    for (int k = 0; k < 64; ++k) { const double a = -(k * (CN_PI / 2 / 16)); cs[k] = cos(a); sn[k] = sin(a); }
+    hipMemcpyToSymbol(HIP_SYMBOL(c_circ_cos), cs, sizeof cs);
+    hipMemcpyToSymbol(HIP_SYMBOL(c_circ_sin), sn, sizeof sn);
+    if (g->plan.total > 160 * 1024) { cn_destroy(g); return set_err(CN_EUNSUPPORTED, "LDS plan exceeds 160 KiB"); }
+    if (g->plan.total > 64 * 1024)
+        hipFuncSetAttribute((const void *)cn_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, g->plan.total);
+    g->rng_grid = g->E < 2048 ? g->E : 2048;
+    HIPCHK(hipDeviceSynchronize());
+    *out = g;
+    return CN_OK;
+}
+
+void cn_destroy(cn_engine *g)
+{
+    if (!g) return;
+    hipSetDevice(g->device);
+    hipFree(g->state);
+    hipFree(g->work);
+    hipFree(g->work_count);
+    delete g;
+}
+
+int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, float *spatial)
+{
+    if (!g || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    RngArgs a;
+    a.s = g->s; a.work = g->work; a.work_count = g->work_count; a.reset_all = 1; a.E = g->E;
+    a.case_size = g->case_size; a.counter_offset = g->counter_offset;
+    a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
+    hipLaunchKernelGGL(cn_rng_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
+
+int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node, float *temporal, float *spatial,
+            float *reward, uint8_t *done, int8_t *event, float *info, double *ep_return, int32_t *ep_len)
+{
+    if (!g || !actions || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    HIPCHK(hipMemsetAsync(g->work_count, 0, 16, st));
+    StepArgs a;
+    a.s = g->s; a.actions = actions; a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
+    a.reward = reward; a.done = done; a.event = event; a.info = info; a.ep_return = ep_return; a.ep_len = ep_len;
+    a.work = g->work; a.work_count = g->work_count; a.E = g->E;
+    const int blocks = (g->E + g->plan.EPB - 1) / g->plan.EPB;
+    hipLaunchKernelGGL(cn_step_kernel, dim3(blocks), dim3(CN_BLK), g->plan.total, st, a, g->c);
+    HIPCHK(hipGetLastError());
+    RngArgs b;
+    b.s = g->s; b.work = g->work; b.work_count = g->work_count; b.reset_all = 0; b.E = g->E;
+    b.case_size = g->case_size; b.counter_offset = g->counter_offset;
+    b.robot_node = robot_node; b.temporal = temporal; b.spatial = spatial;
+    hipLaunchKernelGGL(cn_rng_kernel, dim3(g->rng_grid), dim3(64), 0, st, b, g->c);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
+
+int cn_state_bytes(const cn_engine *g, int64_t *bytes)
+{
+    if (!g || !bytes) return set_err(CN_EINVAL, "null argument");
+    *bytes = g->state_bytes;
+    return CN_OK;
+}
+
+const void *cn_state_device_ptr(const cn_engine *g) { return g ? g->state : nullptr; }
+
+int cn_get_state(cn_engine *g, void *stream, void *dst, int dst_on_host)
+{
+    if (!g || !dst) return set_err(CN_EINVAL, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (dst_on_host) {
+        HIPCHK(hipMemcpyAsync(dst, g->state, g->state_bytes, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    } else {
+        HIPCHK(hipMemcpyAsync(dst, g->state, g->state_bytes, hipMemcpyDeviceToDevice, st));
+    }
+    return CN_OK;
+}
+
+int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
+{
+    if (!g || !src) return set_err(CN_EINVAL, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (src_on_host) {
+        HIPCHK(hipMemcpyAsync(g->state, src, g->state_bytes, hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+    } else {
+        HIPCHK(hipMemcpyAsync(g->state, src, g->state_bytes, hipMemcpyDeviceToDevice, st));
+    }
+    return CN_OK;
+}
+
+int cn_edge_features(void *stream, int64_t E, int N, const float *robot_node, const float *temporal_edges,
+                     const float *spatial_edges, const float *Wt, const float *bt, const float *Ws, const float *bs,
+                     const float *Wr, const float *br, const float *Wn, const float *bn, float *temporal_embed,
+                     float *spatial_embed, float *node_embed)
+{
+    if (E <= 0 || N <= 0) return set_err(CN_EINVAL, "E, N must be > 0");
+    const int64_t threads = E * (N + 2) * 16;
+    const int64_t blocks = (threads + 255) / 256;
+    hipLaunchKernelGGL(cn_edge_features_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, E, N,
+                       robot_node, temporal_edges, spatial_edges, Wt, bt, Ws, bs, Wr, br, Wn, bn, temporal_embed,
+                       spatial_embed, node_embed);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,90 @@
+// cn_math.h — numerics shared by the HIP engine kernels (gfx950).
+//
+// The reference computes in numpy 2.2 (NEP 50 scalar promotion) and RVO2 (float32 C++, no FMA
+// contraction). The engine is compiled with -ffp-contract=off and spells out every fused op that the
+// reference itself fuses (numpy's OpenBLAS ddot: np.linalg.norm / np.dot of float64 2-vectors).
+// Division and square roots use the correctly rounded forms.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CN_PI 3.141592653589793
+
+namespace cn {
+
+__device__ __forceinline__ double dsqrt(double x) { return __dsqrt_rn(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __fsqrt_rn(x); }
+__device__ __forceinline__ double ddiv(double a, double b) { return __ddiv_rn(a, b); }
+__device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+
+// np.linalg.norm of a float64 2-vector: sqrt(fma(b, b, a*a))  (OpenBLAS ddot tail loop is fused)
+__device__ __forceinline__ double np_norm2(double a, double b) { return dsqrt(__fma_rn(b, b, a * a)); }
+// np.linalg.norm of a float32 2-vector: plain float32
+__device__ __forceinline__ float np_norm2f(float a, float b) { return fsqrt(a * a + b * b); }
+// np.dot of float64 2-vectors
+__device__ __forceinline__ double np_dot2(double a0, double a1, double b0, double b1) { return __fma_rn(a1, b1, a0 * b0); }
+
+__device__ __forceinline__ double np_mod(double a, double b)
+{
+    double m = fmod(a, b);
+    if (m != 0.0) { if ((b < 0) != (m < 0)) m += b; }
+    else m = copysign(0.0, b);
+    return m;
+}
+__device__ __forceinline__ float np_modf(float a, float b)
+{
+    float m = fmodf(a, b);
+    if (m != 0.0f) { if ((b < 0) != (m < 0)) m += b; }
+    else m = copysignf(0.0f, b);
+    return m;
+}
+
+// numpy 2.x float32 sin/cos (Cody-Waite + minimax polynomials with FMA): np.sin/np.cos on float32
+// scalars in the reference use this, not libm; bit-exact replica (see oracle/cpu_ref.c).
+__device__ inline float np_sincosf(float x, bool want_cos)
+{
+    const float max_cody = want_cos ? 71476.0625f : 117435.992f;
+    if (!(fabsf(x) <= max_cody)) return want_cos ? cosf(x) : sinf(x);
+    float q = x * 0x1.45f306p-1f;
+    q = q + 0x1.800000p+23f;
+    q = q - 0x1.800000p+23f;
+    float r = __fmaf_rn(q, -0x1.921fb0p+00f, x);
+    r = __fmaf_rn(q, -0x1.5110b4p-22f, r);
+    r = __fmaf_rn(q, -0x1.846988p-48f, r);
+    const float r2 = r * r;
+    float c = __fmaf_rn(0x1.98e616p-16f, r2, -0x1.6c06dcp-10f);
+    c = __fmaf_rn(c, r2, 0x1.55553cp-05f);
+    c = __fmaf_rn(c, r2, -0x1.000000p-01f);
+    c = __fmaf_rn(c, r2, 0x1.000000p+00f);
+    float s = __fmaf_rn(0x1.7d3bbcp-19f, r2, -0x1.a06bbap-13f);
+    s = __fmaf_rn(s, r2, 0x1.11119ap-07f);
+    s = __fmaf_rn(s, r2, -0x1.555556p-03f);
+    s = __fmaf_rn(s, r2, 0.0f);
+    s = __fmaf_rn(s, r, r);
+    const int iq = (int)q + (want_cos ? 1 : 0);
+    float out = (iq & 1) == 0 ? s : c;
+    if ((iq & 2) == 2) out = 0.0f - out;
+    return out;
+}
+__device__ __forceinline__ float np_sinf(float x) { return np_sincosf(x, false); }
+__device__ __forceinline__ float np_cosf(float x) { return np_sincosf(x, true); }
+__device__ __forceinline__ float np_clipf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// ---------------------------------------------------------------------------------------------
+// numpy legacy MT19937 (mt19937_seed / mt19937_gen / mt19937_next / mt19937_next_double)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y)
+{
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c)
+{
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return c ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
+}
+
+}  // namespace cn

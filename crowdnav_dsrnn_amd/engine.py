@@ -1,0 +1,130 @@
+"""Device-resident batched CrowdSimDict engine (torch tensors in, torch tensors out).
+
+Thin host wrapper over the C ABI (include/crowdnav.h, crowdnav_dsrnn_amd/csrc/cn_engine.hip): it
+owns the output buffers (torch, on the engine's device) and passes `data_ptr()`s and the current
+torch stream to `cn_reset` / `cn_step`. No compute happens here and there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib, abi
+
+
+class CrowdNavEngine:
+    """E environments of the reference's CrowdSimDict on one GPU.
+
+    reset()                  -> obs dict (robot_node (E,1,7), temporal_edges (E,1,2), spatial_edges (E,N,2))
+    step(actions (E,2) f32)  -> obs, reward (E,), done (E,) bool, event (E,) int8, info (E,K), ep_return (E,) f64,
+                                ep_len (E,) i32       (auto-reset of finished envs, like the reference VecEnv)
+    Returned tensors are the engine's own buffers (overwritten by the next call); clone to keep them.
+    """
+
+    def __init__(self, cfg, device=None):
+        import torch
+
+        self.torch = torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("CrowdNavEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.cfg = cfg.copy()
+        self.E, self.N = int(cfg.num_envs), int(cfg.human_num)
+        self.device = torch.device(device if device is not None else "cuda:%d" % torch.cuda.current_device())
+        L = _lib.lib()
+        _lib.check(L.cn_config_validate(ctypes.byref(self.cfg)))
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(L.cn_create(ctypes.byref(self.cfg), self.device.index, ctypes.byref(h)))
+        self._h = h
+        nb = ctypes.c_int64()
+        _lib.check(L.cn_state_bytes(h, ctypes.byref(nb)))
+        self.state_bytes = nb.value
+        E, N, dev = self.E, self.N, self.device
+        self.robot_node = torch.zeros((E, 1, 7), dtype=torch.float32, device=dev)
+        self.temporal_edges = torch.zeros((E, 1, 2), dtype=torch.float32, device=dev)
+        self.spatial_edges = torch.zeros((E, N, 2), dtype=torch.float32, device=dev)
+        self.reward = torch.zeros((E,), dtype=torch.float32, device=dev)
+        self.done = torch.zeros((E,), dtype=torch.uint8, device=dev)
+        self.event = torch.zeros((E,), dtype=torch.int8, device=dev)
+        self.info = torch.zeros((E, abi.INFO_K), dtype=torch.float32, device=dev)
+        self.ep_return = torch.zeros((E,), dtype=torch.float64, device=dev)
+        self.ep_len = torch.zeros((E,), dtype=torch.int32, device=dev)
+
+    # -------------------------------------------------------------------------------------------
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def obs(self):
+        return {"robot_node": self.robot_node, "temporal_edges": self.temporal_edges,
+                "spatial_edges": self.spatial_edges}
+
+    def reset(self):
+        with self.torch.cuda.device(self.device):
+            _lib.check(_lib.lib().cn_reset(self._h, self._stream(), self.robot_node.data_ptr(),
+                                           self.temporal_edges.data_ptr(), self.spatial_edges.data_ptr()))
+        return self.obs()
+
+    def step(self, actions):
+        t = self.torch
+        if actions.device != self.device or actions.dtype != t.float32 or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=t.float32).contiguous()
+        if actions.numel() != self.E * 2:
+            raise ValueError("actions must have E*2 = %d elements, got %d" % (self.E * 2, actions.numel()))
+        with t.cuda.device(self.device):
+            _lib.check(_lib.lib().cn_step(
+                self._h, self._stream(), actions.data_ptr(), self.robot_node.data_ptr(),
+                self.temporal_edges.data_ptr(), self.spatial_edges.data_ptr(), self.reward.data_ptr(),
+                self.done.data_ptr(), self.event.data_ptr(), self.info.data_ptr(), self.ep_return.data_ptr(),
+                self.ep_len.data_ptr()))
+        return self.obs(), self.reward, self.done.bool(), self.event, self.info, self.ep_return, self.ep_len
+
+    # -------------------------------------------------------------------------------------------
+    def get_state(self):
+        buf = np.zeros(self.state_bytes, np.uint8)
+        with self.torch.cuda.device(self.device):
+            _lib.check(_lib.lib().cn_get_state(self._h, self._stream(), buf.ctypes.data_as(ctypes.c_void_p), 1))
+        return abi.StateView(buf, self.E, self.N, self.cfg.robot_visible)
+
+    def set_state(self, sv):
+        blob = np.ascontiguousarray(sv.blob)
+        if blob.nbytes != self.state_bytes:
+            raise ValueError("state blob has %d bytes, engine expects %d" % (blob.nbytes, self.state_bytes))
+        with self.torch.cuda.device(self.device):
+            _lib.check(_lib.lib().cn_set_state(self._h, self._stream(), blob.ctypes.data_as(ctypes.c_void_p), 1))
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            _lib.lib().cn_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class NumpyEngine:
+    """numpy-in/numpy-out facade over CrowdNavEngine with the oracle's interface (used by tests)."""
+
+    def __init__(self, cfg, device=None):
+        self.eng = CrowdNavEngine(cfg, device)
+        self.E, self.N = self.eng.E, self.eng.N
+
+    def reset(self):
+        o = self.eng.reset()
+        self.eng.torch.cuda.synchronize(self.eng.device)
+        return {k: v.cpu().numpy() for k, v in o.items()}
+
+    def step(self, actions):
+        t = self.eng.torch
+        a = t.from_numpy(np.ascontiguousarray(actions, np.float32).reshape(self.E, 2)).to(self.eng.device)
+        obs, rew, done, ev, info, epr, epl = self.eng.step(a)
+        t.cuda.synchronize(self.eng.device)
+        return ({k: v.cpu().numpy() for k, v in obs.items()}, rew.cpu().numpy(), done.cpu().numpy(),
+                ev.cpu().numpy(), info.cpu().numpy(), epr.cpu().numpy(), epl.cpu().numpy())
+
+    def get_state(self):
+        return self.eng.get_state()
+
+    def set_state(self, sv):
+        self.eng.set_state(sv)

@@ -1,0 +1,178 @@
+/*
+ * crowdnav.h — C ABI of the MI355X batched CrowdSimDict engine (libcrowdnav_hip.so).
+ *
+ * Drop-in boundary for the reference's env hot path. Each entry point replaces a reference
+ * interface (paths relative to the CrowdNav_DSRNN checkout):
+ *
+ *   cn_create     ⟵ gym.make('CrowdSimDict-v0') + CrowdSim.configure(config) + make_env's
+ *                   thisSeed/nenv/phase assignment, for E envs at once
+ *                   (crowd_sim/__init__.py:9-11, crowd_sim/envs/crowd_sim.py:93-246,
+ *                    pytorchBaselines/a2c_ppo_acktr/envs.py:46-75)
+ *   cn_reset      ⟵ CrowdSimDict.reset() of every env (crowd_sim/envs/crowd_sim_dict.py:105-203),
+ *                   i.e. ShmemVecEnv.reset (shmem_vec_env.py:89-95) + VecPyTorch.reset (envs.py:215-222)
+ *   cn_step       ⟵ CrowdSimDict.step(action) of every env (crowd_sim_dict.py:205-271) followed by the
+ *                   VecEnv worker's auto-reset (shmem_vec_env.py:164-168) and bench.Monitor's episode
+ *                   bookkeeping; i.e. VecPyTorch.step (envs.py:224-239) minus the Python info dicts
+ *   cn_get_state / cn_set_state   ⟵ no reference equivalent (state lives in forked workers there);
+ *                   used for teacher-forced parity tests and rollout checkpointing
+ *   cn_edge_features ⟵ the input layers of the DSRNN forward, fused:
+ *                   HumanHumanEdgeRNN.encoder_linear+ReLU (srnn_model.py:210-211) for the temporal and
+ *                   spatial edges, SRNN.robot_linear (srnn_model.py:466) and
+ *                   HumanNodeRNN.encoder_linear+ReLU (srnn_model.py:160-161)
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (torch tensors' data_ptr()), row-major, caller-owned.
+ *   - `stream` is a hipStream_t passed as void* (NULL = legacy default stream). Calls are
+ *     stream-ordered and asynchronous; no call allocates or synchronises except cn_create/cn_destroy
+ *     and the host-copy variants of get/set_state.
+ *   - Every call returns 0 on success or a negative CN_E* code; cn_last_error() gives a message
+ *     (thread-local). Unsupported reference options are rejected by cn_create with CN_EUNSUPPORTED.
+ */
+#ifndef CROWDNAV_H
+#define CROWDNAV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* error codes */
+#define CN_OK 0
+#define CN_EINVAL (-1)
+#define CN_EUNSUPPORTED (-2)
+#define CN_EHIP (-3)
+#define CN_ENOMEM (-4)
+
+/* robot kinematics  (config.action_space.kinematics, crowd_nav/configs/config.py:137) */
+#define CN_HOLONOMIC 0
+#define CN_UNICYCLE 1
+/* human policies    (policy_factory, crowd_nav/policy/policy_factory.py:1-17) */
+#define CN_POLICY_ORCA 0
+#define CN_POLICY_SOCIAL_FORCE 1
+/* phases            (crowd_sim.py:110-119, 690-694) */
+#define CN_PHASE_TRAIN 0
+#define CN_PHASE_VAL 1
+#define CN_PHASE_TEST 2
+/* scenarios         (create_agent_attributes, crowd_sim.py:296-357) */
+#define CN_SC_CIRCLE_CROSSING 0
+#define CN_SC_SQUARE_CROSSING 1
+#define CN_SC_PARALLEL_TRAFFIC 2
+#define CN_SC_PERPENDICULAR_TRAFFIC 3
+#define CN_SC_SIDE_PREF_PASSING 4
+#define CN_SC_SIDE_PREF_OVERTAKING 5
+#define CN_SC_SIDE_PREF_CROSSING 6
+/* scenario selection at reset (crowd_sim_dict.py:110-125) */
+#define CN_SCMODE_ROUND_ROBIN 0  /* env g uses scenarios[g % n]; n == 1 is the deterministic reference case */
+#define CN_SCMODE_SEQUENTIAL 1   /* test.social_metrics: scenarios[reset_count % n] (crowd_sim_dict.py:114-122) */
+/* step events (crowd_sim/envs/utils/info.py) */
+#define CN_EV_NOTHING 0
+#define CN_EV_DANGER 1
+#define CN_EV_COLLISION 2
+#define CN_EV_REACHGOAL 3
+#define CN_EV_TIMEOUT 4
+
+/* per-step info metrics, float32 [E][CN_INFO_K]  (step_info keys, crowd_sim.py:973-1030) */
+#define CN_INFO_AGG_NAV_TIME 0
+#define CN_INFO_PATH_VIOLATION 1
+#define CN_INFO_PERSONAL_VIOLATION 2
+#define CN_INFO_JERK_COST 3
+#define CN_INFO_DIST_TO_GOAL 4
+#define CN_INFO_SPEED_VIOLATION 5
+#define CN_INFO_MIN_DIST 6     /* Danger(min_dist) payload; dmin (inf if no human counted) */
+#define CN_INFO_SCENARIO 7
+#define CN_INFO_SIDE_LEFT 8    /* test.side_preference only (crowd_sim.py:977-992) */
+#define CN_INFO_SIDE_RIGHT 9
+#define CN_INFO_SEPARATION 10
+#define CN_INFO_OVERFLOW 11    /* bounded-rejection overflows so far in this episode (engine diagnostic) */
+#define CN_INFO_K 12
+
+#define CN_MAX_SCENARIOS 8
+
+typedef struct cn_config {
+    /* batch geometry */
+    int32_t num_envs;      /* E: envs owned by this engine instance (one device) */
+    int32_t human_num;     /* N: config.sim.human_num */
+    int64_t env_offset;    /* global index of local env 0 (sharding); thisSeed = seed + global index */
+    int64_t nenv;          /* the reference's env.nenv = num_processes over ALL shards (envs.py:69) */
+    int64_t seed;          /* config.env.seed (envs.py:66) */
+    int32_t phase;         /* CN_PHASE_*; make_env uses 'train' if nenv > 1 else 'test' (envs.py:70-73) */
+    int32_t kinematics;    /* CN_HOLONOMIC / CN_UNICYCLE */
+    int32_t human_policy;  /* CN_POLICY_* */
+    int32_t scenario_mode; /* CN_SCMODE_* */
+    int32_t num_scenarios;
+    int32_t scenarios[CN_MAX_SCENARIOS];
+    int32_t val_size, test_size;          /* config.env.val_size / test_size (case_size) */
+    /* env (config.env / config.sim) */
+    double time_step, time_limit, circle_radius, square_width;
+    /* agents */
+    double robot_radius, robot_vpref, robot_fov; /* fov in radians = pi * config.robot.FOV */
+    double human_radius, human_vpref, human_fov;
+    int32_t robot_visible, randomize_attributes;
+    int32_t random_goal_changing, end_goal_changing, random_radii, random_v_pref;
+    double goal_change_chance, end_goal_change_chance;
+    /* reward (config.reward) */
+    double success_reward, collision_penalty, discomfort_dist, discomfort_penalty_factor;
+    double potential_factor, norm_zone_penalty;
+    int32_t potential_based, time_factor, norm_zones, norm_zone_lhs;
+    /* social (config.social / config.test) */
+    double min_personal_space, max_walking_speed;
+    int32_t social_metrics, side_preference;
+    /* human policies (config.orca / config.sf) */
+    double orca_neighbor_dist, orca_safety_space, orca_time_horizon, orca_time_horizon_obst;
+    double sf_A, sf_B, sf_KI;
+    /* engine */
+    int32_t max_tries;     /* bounded rejection sampling (reference loops forever) */
+    int32_t reserved;
+} cn_config;
+
+typedef struct cn_engine cn_engine;
+
+const char *cn_last_error(void);
+const char *cn_version(void);
+
+int cn_config_validate(const cn_config *cfg);
+int cn_create(const cn_config *cfg, int device, cn_engine **out);
+void cn_destroy(cn_engine *eng);
+
+/* Reset all envs (fresh episodes, case_counter continues). obs out: robot_node [E][7], temporal [E][2],
+ * spatial [E][N][2] float32. */
+int cn_reset(cn_engine *eng, void *stream, float *robot_node, float *temporal_edges, float *spatial_edges);
+
+/* One step of every env with auto-reset of finished envs.
+ * in : actions [E][2] float32 (raw policy output; clipped in place semantics of SRNN.clip_action are
+ *      NOT applied to the caller's buffer — the reference mutates its private numpy copy)
+ * out: obs (first obs of the new episode where done), reward [E] f32, done [E] u8, event [E] i8,
+ *      info [E][CN_INFO_K] f32, ep_return [E] f64 and ep_len [E] i32 (Monitor 'r'/'l', valid where done).
+ * Any output pointer except the obs may be NULL. */
+int cn_step(cn_engine *eng, void *stream, const float *actions,
+            float *robot_node, float *temporal_edges, float *spatial_edges,
+            float *reward, uint8_t *done, int8_t *event, float *info,
+            double *ep_return, int32_t *ep_len);
+
+/* State blob (layout: include/crowdnav_state.h). */
+int cn_state_bytes(const cn_engine *eng, int64_t *bytes);
+int cn_state_layout_offsets(const cn_config *cfg, int64_t *offsets, int64_t *total_bytes);
+int cn_state_field_info(int field, const char **name, int *type_code, int *count_kind);
+int cn_get_state(cn_engine *eng, void *stream, void *dst, int dst_on_host);
+int cn_set_state(cn_engine *eng, void *stream, const void *src, int src_on_host);
+const void *cn_state_device_ptr(const cn_engine *eng);
+
+/* Fused DSRNN edge-feature assembly (SRNN input layers), float32, device pointers.
+ *   robot_node [E][7], temporal [E][2], spatial [E][N][2]
+ *   Wt [64][2] bt[64]  (humanhumanEdgeRNN_temporal.encoder_linear)
+ *   Ws [64][2] bs[64]  (humanhumanEdgeRNN_spatial.encoder_linear)
+ *   Wr [3][7]  br[3]   (robot_linear)
+ *   Wn [64][3] bn[64]  (humanNodeRNN.encoder_linear)
+ * out: temporal_embed [E][64], spatial_embed [E][N][64], node_embed [E][64]  (post-ReLU) */
+int cn_edge_features(void *stream, int64_t E, int N,
+                     const float *robot_node, const float *temporal_edges, const float *spatial_edges,
+                     const float *Wt, const float *bt, const float *Ws, const float *bs,
+                     const float *Wr, const float *br, const float *Wn, const float *bn,
+                     float *temporal_embed, float *spatial_embed, float *node_embed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CROWDNAV_H */

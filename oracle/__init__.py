@@ -1,0 +1,5 @@
+"""CPU oracle for the CrowdSimDict hot path — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this package, and
+only as the checker or the timed CPU baseline. The product (crowdnav_dsrnn_amd) never imports it.
+"""

@@ -1,0 +1,510 @@
+"""Generate golden vectors from the REFERENCE implementation (run in the build container only).
+
+    python oracle/gen_golden.py [--out tests/golden]
+
+Imports the reference's own code from /root/reference (read-only) through the shims in
+oracle/shims (gym, shapely, rvo2, torchvision — see oracle/shims/README.md) and records:
+
+  spawn_*.npz    CrowdSimDict.reset() states for the reference seed schedule
+                 (crowd_sim_dict.py:105-203, crowd_sim.py:555-663, 296-393)
+  roll_*.npz     teacher-forced step sequences: per step the actions, the post-step state, the
+                 observation, reward, done, event, info — with the VecEnv worker's auto-reset
+                 (shmem_vec_env.py:164-168) and bench.Monitor's episode return
+  dsrnn.npz      DSRNN Policy.act / evaluate_actions with procedural weights
+                 (pytorchBaselines/a2c_ppo_acktr/model.py:63-104, srnn_model.py:409-504)
+
+The fixtures are data only (inputs and expected outputs); nothing of the reference's source is
+copied. The reference never travels to the GPU box; these .npz files do.
+Deviations applied to the reference while recording (each documented in DESIGN.md):
+  - unicycle: ActionRot gets vx/vy = commanded world-frame velocity so calc_reward's jerk/speed
+    metrics do not raise (crowd_sim.py:1004 reads action.vx);
+  - the ORCA frozen-simulator parameters are read back from the rvo2 shim into the state.
+"""
+import argparse
+import math
+import os
+import sys
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+REF = "/root/reference"
+sys.path[:0] = [os.path.join(HERE, "shims"), REF, REPO]
+
+from crowdnav_dsrnn_amd import abi  # noqa: E402
+from crowdnav_dsrnn_amd.config import clone_config  # noqa: E402
+
+# ---- reference imports (through the shims) ----
+import crowd_sim.envs.utils.action as ref_action  # noqa: E402
+
+_CUR = {"theta": 0.0}
+
+
+class ActionRotV(ref_action.ActionRot):
+    """ActionRot + the commanded world-frame velocity (SURVEY §9-1 patch; metrics only)."""
+
+    @property
+    def vx(self):
+        th = (self._theta() + self.r) % (2 * np.pi)
+        return self.v * np.cos(th)
+
+    @property
+    def vy(self):
+        th = (self._theta() + self.r) % (2 * np.pi)
+        return self.v * np.sin(th)
+
+    def _theta(self):
+        return _CUR["theta"]
+
+
+ref_action.ActionRot = ActionRotV
+
+from crowd_nav.configs.config import Config as RefConfig  # noqa: E402
+from crowd_nav.policy import orca as ref_orca  # noqa: E402
+from crowd_sim.envs import crowd_sim as ref_crowd_sim  # noqa: E402
+from crowd_sim.envs import crowd_sim_dict as ref_csd  # noqa: E402
+from crowd_sim.envs.utils import info as ref_info  # noqa: E402
+
+ref_csd.ActionRot = ActionRotV
+import crowd_nav.policy.srnn as ref_srnn  # noqa: E402
+
+ref_srnn.ActionRot = ActionRotV
+
+_orig_calc_reward = ref_crowd_sim.CrowdSim.calc_reward
+
+
+def _calc_reward(self, action):
+    _CUR["theta"] = self.robot.theta
+    return _orig_calc_reward(self, action)
+
+
+ref_crowd_sim.CrowdSim.calc_reward = _calc_reward
+
+# record which observed slots were dummies when each human's RVO2 simulator was created
+_orig_predict = ref_orca.ORCA.predict
+
+
+def _predict(self, state):
+    creating = self.sim is None
+    out = _orig_predict(self, state)
+    if creating:
+        self.dummy_mask = 0
+        for k, hs in enumerate(state.human_states):
+            if hs.px == 7 and hs.py == 7 and hs.vx == 0 and hs.vy == 0:
+                self.dummy_mask |= 1 << k
+    return out
+
+
+ref_orca.ORCA.predict = _predict
+
+EVENT_CODE = {ref_info.Nothing: 0, ref_info.Danger: 1, ref_info.Collision: 2, ref_info.ReachGoal: 3,
+              ref_info.Timeout: 4}
+
+
+def make_ref_config(kin="holonomic", policy="orca", scenarios=("circle_crossing",), N=5, fov_robot=2.0,
+                    fov_human=2.0, side_pref=False, norm_zones=False, social_metrics=False, robot_visible=False,
+                    random_radii=False, random_v_pref=False, time_factor=False, time_step=0.25):
+    c = clone_config(RefConfig())
+    c.action_space.kinematics = kin
+    c.humans.policy = policy
+    c.sim.train_val_sim = list(scenarios)
+    c.sim.test_sim = list(scenarios)
+    c.sim.human_num = N
+    c.robot.FOV = fov_robot
+    c.humans.FOV = fov_human
+    c.test.side_preference = side_pref
+    c.test.social_metrics = social_metrics
+    c.robot.visible = robot_visible
+    c.humans.random_radii = random_radii
+    c.humans.random_v_pref = random_v_pref
+    c.reward.time_factor = time_factor
+    c.env.time_step = time_step
+    c.reward.discomfort_penalty_factor = 10 * time_step
+    if side_pref:
+        c.sim.circle_radius = 4
+        c.humans.random_goal_changing = False
+        c.humans.end_goal_changing = False
+    c.reward.norm_zones = norm_zones
+    return c
+
+
+def make_ref_env(cfg, this_seed, nenv):
+    env = ref_csd.CrowdSimDict()
+    env.configure(cfg)
+    env.thisSeed = this_seed
+    env.nenv = nenv
+    env.phase = "train" if nenv > 1 else "test"
+    env.ep_ret, env.ep_len = 0.0, 0
+    return env
+
+
+def extract(envs, cfg):
+    """Reference env objects -> abi.StateView (every field of include/crowdnav_state.h)."""
+    E, N = len(envs), cfg.sim.human_num
+    sv = abi.StateView(None, E, N, cfg.robot.visible)
+    A = abi.sim_agents(N, cfg.robot.visible)
+    for e, env in enumerate(envs):
+        r = env.robot
+        for f, v in (("r_px", r.px), ("r_py", r.py), ("r_gx", r.gx), ("r_gy", r.gy), ("r_vx", r.vx),
+                     ("r_vy", r.vy), ("r_theta", r.theta), ("r_dv", env.desiredVelocity[0]),
+                     ("r_radius", r.radius), ("r_vpref", r.v_pref), ("potential", env.potential),
+                     ("gtime", env.global_time), ("last_ax", env.last_acceleration[0]),
+                     ("last_ay", env.last_acceleration[1]), ("ep_return", env.ep_ret)):
+            getattr(sv, f)[e] = float(v)
+        sv.case_counter[e] = env.case_counter[env.phase]
+        sv.ep_len[e] = env.ep_len
+        sv.scenario[e] = abi.SCENARIO_ID[env.current_scenario]
+        sv.reset_count[e] = env.scenario_counter
+        frozen = cfg.humans.policy == "orca" and env.humans[0].policy.sim is not None
+        nan = any(not (math.isfinite(h.px) and math.isfinite(h.py)) for h in env.humans)
+        rf32 = isinstance(r.vx, np.float32)
+        sv.flags[e] = ((abi.FLAG_ORCA_FROZEN if frozen else 0) | (abi.FLAG_NAN if nan else 0) |
+                       (abi.FLAG_ROBOT_F32 if rf32 else 0))
+        st = env.rng_state
+        sv.mt[e] = st[1]
+        sv.mt_pos[e] = st[2]
+        for i, h in enumerate(env.humans):
+            for f, v in (("h_px", h.px), ("h_py", h.py), ("h_gx", h.gx), ("h_gy", h.gy), ("h_vx", h.vx),
+                         ("h_vy", h.vy), ("h_r", h.radius), ("h_vpref", h.v_pref), ("h_theta", h.theta)):
+                getattr(sv, f)[e, i] = float(v)
+            sv.b_px[e, i], sv.b_py[e, i], sv.b_vx[e, i], sv.b_vy[e, i], sv.b_r[e, i] = env.last_human_states[i]
+            if frozen:
+                sim = h.policy.sim
+                sv.o_r[e, i] = sim.agents[0].radius
+                sv.o_vmax[e, i] = sim.agents[0].maxSpeed
+                sv.o_dmask[e, i] = h.policy.dummy_mask
+                if A > 10:
+                    sv.o_perm[e, i * A:(i + 1) * A] = sim.kd_agents
+    return sv
+
+
+# Each reference env owns the process-global np.random stream while it runs (one env per process in
+# the reference's ShmemVecEnv); we swap the stream in and out around every call.
+_ACTIVE = {"env": None}
+
+
+class _ScenarioChoice(object):
+    """Replaces the unseeded `random.choices` of crowd_sim_dict.py:125 with the engine's deterministic
+    assignment (global env index round-robin); identical to the reference for one scenario."""
+
+    @staticmethod
+    def choices(seq, weights=None):
+        return [seq[_CUR["gidx"] % len(seq)]]
+
+
+ref_csd.random = _ScenarioChoice
+
+
+def run_in(env, fn, *a):
+    _CUR["gidx"] = env.thisSeed
+    if getattr(env, "rng_state", None) is not None:
+        np.random.set_state(env.rng_state)
+    _ACTIVE["env"] = env
+    out = fn(*a)
+    env.rng_state = np.random.get_state()
+    _ACTIVE["env"] = None
+    return out
+
+
+def obs32(ob):
+    return (np.asarray(ob["robot_node"], np.float32).reshape(1, 7),
+            np.asarray(ob["temporal_edges"], np.float32).reshape(1, 2),
+            np.asarray(ob["spatial_edges"], np.float32))
+
+
+def env_reset(env):
+    ob = run_in(env, env.reset)
+    env.ep_ret, env.ep_len = 0.0, 0
+    return ob
+
+
+def env_step(env, action):
+    a = np.array(action, dtype=np.float32)
+    ob, rew, done, info = run_in(env, env.step, a)
+    env.ep_ret += rew  # bench.Monitor: sum(self.rewards)
+    env.ep_len += 1
+    ep = (env.ep_ret, env.ep_len)
+    if done:
+        ob = env_reset(env)
+    return ob, rew, done, info, ep
+
+
+def info_vec(info, scenario):
+    si = info["info"]
+    v = np.zeros(abi.INFO_K, np.float32)
+    v[abi.INFO_AGG_NAV_TIME] = si["aggregate_nav_time"]
+    v[abi.INFO_PATH_VIOLATION] = si["path_violation"]
+    v[abi.INFO_PERSONAL_VIOLATION] = si["personal_violation"]
+    v[abi.INFO_JERK_COST] = si["jerk_cost"]
+    v[abi.INFO_DIST_TO_GOAL] = si["dist_to_goal"]
+    v[abi.INFO_SPEED_VIOLATION] = si["speed_violation"]
+    ev = si["event"]
+    v[abi.INFO_MIN_DIST] = ev.min_dist if isinstance(ev, ref_info.Danger) else np.nan
+    v[abi.INFO_SCENARIO] = abi.SCENARIO_ID[si["scenario"]]
+    if scenario in si:
+        v[abi.INFO_SIDE_LEFT] = si[scenario]["left"]
+        v[abi.INFO_SIDE_RIGHT] = si[scenario]["right"]
+        v[abi.INFO_SEPARATION] = si["separation"]
+    return v, EVENT_CODE[type(ev)]
+
+
+def cfg_meta(cfg, E):
+    return dict(kinematics=cfg.action_space.kinematics, policy=cfg.humans.policy, N=cfg.sim.human_num, E=E,
+                scenarios=",".join(cfg.sim.train_val_sim), robot_fov=cfg.robot.FOV, human_fov=cfg.humans.FOV,
+                side_pref=int(cfg.test.side_preference), norm_zones=int(cfg.reward.norm_zones),
+                social_metrics=int(cfg.test.social_metrics), robot_visible=int(cfg.robot.visible),
+                random_radii=int(cfg.humans.random_radii), random_v_pref=int(cfg.humans.random_v_pref),
+                time_factor=int(cfg.reward.time_factor), time_step=cfg.env.time_step,
+                circle_radius=cfg.sim.circle_radius)
+
+
+def pack_state(sv, prefix, out, with_mt):
+    for name, _, _ in abi.STATE_FIELDS:
+        if name == "mt" and not with_mt:
+            continue
+        out[prefix + name] = np.array(getattr(sv, name))
+    out[prefix + "mt_crc"] = np.array([zlib.crc32(np.ascontiguousarray(sv.mt[e]).tobytes())
+                                       for e in range(sv.E)], np.uint32)
+
+
+def gen_spawn(name, cfg, E, resets, outdir):
+    nenv = E
+    envs = [make_ref_env(cfg, r, nenv) for r in range(E)]
+    out = {"meta_" + k: np.array(v) for k, v in cfg_meta(cfg, E).items()}
+    for k in range(resets):
+        # start from a blank state carrying only the case counters (all the reset reads)
+        pre = extract_pre_reset(envs, cfg)
+        obs = [obs32(env_reset(env)) for env in envs]
+        post = extract(envs, cfg)
+        pack_state(pre, "k%d_pre_" % k, out, True)
+        pack_state(post, "k%d_post_" % k, out, False)
+        out["k%d_robot_node" % k] = np.stack([o[0] for o in obs])
+        out["k%d_temporal" % k] = np.stack([o[1] for o in obs])
+        out["k%d_spatial" % k] = np.stack([o[2] for o in obs])
+    out["resets"] = np.array(resets)
+    np.savez_compressed(os.path.join(outdir, "spawn_%s.npz" % name), **out)
+    print("spawn", name, "ok")
+
+
+def extract_pre_reset(envs, cfg):
+    E, N = len(envs), cfg.sim.human_num
+    sv = abi.StateView(None, E, N, cfg.robot.visible)
+    for e, env in enumerate(envs):
+        sv.case_counter[e] = env.case_counter[env.phase]
+        sv.reset_count[e] = env.scenario_counter
+    return sv
+
+
+def goal_action(env, kin, rng):
+    r = env.robot
+    dx, dy = r.gx - r.px, r.gy - r.py
+    d = math.hypot(dx, dy) + 1e-9
+    if kin == "holonomic":
+        return np.array([dx / d * 1.2, dy / d * 1.2], np.float32) + rng.normal(0, 0.05, 2).astype(np.float32)
+    want = math.atan2(dy, dx)
+    dth = (want - r.theta + math.pi) % (2 * math.pi) - math.pi
+    return np.array([0.12, np.clip(dth, -0.15, 0.15)], np.float32)
+
+
+def gen_roll(name, cfg, E, T, outdir, seed=1, goal_frac=0.5):
+    nenv = E
+    kin = cfg.action_space.kinematics
+    envs = [make_ref_env(cfg, r, nenv) for r in range(E)]
+    for env in envs:
+        env_reset(env)
+    rng = np.random.RandomState(seed)
+    out = {"meta_" + k: np.array(v) for k, v in cfg_meta(cfg, E).items()}
+    pack_state(extract(envs, cfg), "init_", out, True)
+    acts = np.zeros((T, E, 2), np.float32)
+    keys = ["robot_node", "temporal", "spatial", "reward", "done", "event", "info", "ep_return", "ep_len"]
+    rec = {k: [] for k in keys}
+    posts = []
+    for t in range(T):
+        for e, env in enumerate(envs):
+            if e < int(E * goal_frac):
+                acts[t, e] = goal_action(env, kin, rng)
+            elif kin == "holonomic":
+                acts[t, e] = rng.normal(0, 0.7, 2).astype(np.float32)
+            else:
+                acts[t, e] = rng.uniform(-0.15, 0.15, 2).astype(np.float32)
+        step_out = []
+        for e, env in enumerate(envs):
+            sc = env.current_scenario
+            ob, rew, done, info, ep = env_step(env, acts[t, e].copy())
+            iv, ev = info_vec(info, sc)
+            step_out.append((obs32(ob), rew, done, ev, iv, ep))
+        rec["robot_node"].append(np.stack([s[0][0] for s in step_out]))
+        rec["temporal"].append(np.stack([s[0][1] for s in step_out]))
+        rec["spatial"].append(np.stack([s[0][2] for s in step_out]))
+        rec["reward"].append(np.array([np.float32(s[1]) for s in step_out], np.float32))
+        rec["done"].append(np.array([s[2] for s in step_out], np.uint8))
+        rec["event"].append(np.array([s[3] for s in step_out], np.int8))
+        rec["info"].append(np.stack([s[4] for s in step_out]))
+        rec["ep_return"].append(np.array([s[5][0] for s in step_out], np.float64))
+        rec["ep_len"].append(np.array([s[5][1] for s in step_out], np.int32))
+        posts.append(extract(envs, cfg))
+    out["actions"] = acts
+    for k in keys:
+        out[k] = np.stack(rec[k])
+    for name_, _, _ in abi.STATE_FIELDS:
+        if name_ == "mt":
+            continue
+        out["post_" + name_] = np.stack([np.array(getattr(p, name_)) for p in posts])
+    out["post_mt_crc"] = np.stack([np.array([zlib.crc32(np.ascontiguousarray(p.mt[e]).tobytes())
+                                             for e in range(E)], np.uint32) for p in posts])
+    np.savez_compressed(os.path.join(outdir, "roll_%s.npz" % name), **out)
+    ev = out["event"]
+    print("roll", name, "events:", {k: int((ev == k).sum()) for k in range(5)}, "dones", int(out["done"].sum()))
+
+
+# --------------------------------------------------------------------------------------------------
+# DSRNN forward vectors (procedural weights)
+# --------------------------------------------------------------------------------------------------
+def procedural_state_dict(model):
+    """Deterministic weights: param p (sorted state_dict order) ~ RandomState(1000 + p).uniform(-s, s),
+    s = 1/sqrt(fan_in) (fan_in = last dim, 1 for 1-D params). Reproducible without files."""
+    import torch
+
+    sd = model.state_dict()
+    out = {}
+    for p, k in enumerate(sorted(sd.keys())):
+        shape = tuple(sd[k].shape)
+        fan_in = shape[-1] if len(shape) > 1 else 1
+        s = 1.0 / math.sqrt(fan_in)
+        out[k] = torch.from_numpy(np.random.RandomState(1000 + p).uniform(-s, s, shape).astype(np.float32))
+    return out
+
+
+def gen_dsrnn(outdir):
+    import torch
+
+    torch.set_num_threads(4)
+    from pytorchBaselines.a2c_ppo_acktr.model import Policy
+
+    import gym
+
+    out = {}
+    for N in (5, 10):
+        E, T = 4, 8
+        cfg = make_ref_config(N=N)
+        cfg.training.cuda = False
+        cfg.training.num_processes = E
+        cfg.ppo.num_steps = T
+        cfg.ppo.num_mini_batch = 1
+        obs_space = {"robot_node": gym.spaces.Box(-np.inf, np.inf, (1, 7)),
+                     "temporal_edges": gym.spaces.Box(-np.inf, np.inf, (1, 2)),
+                     "spatial_edges": gym.spaces.Box(-np.inf, np.inf, (N, 2))}
+        act_space = gym.spaces.Box(-np.inf, np.inf, (2,))
+        act_space.__class__.__name__  # Box
+        torch.manual_seed(0)
+        pol = Policy(obs_space, act_space, base="srnn", base_kwargs=cfg)
+        pol.load_state_dict(procedural_state_dict(pol))
+        pol.eval()
+        rng = np.random.RandomState(7 + N)
+        # act (infer, seq_len 1)
+        obs = {"robot_node": rng.normal(0, 3, (E, 1, 7)).astype(np.float32),
+               "temporal_edges": rng.normal(0, 0.5, (E, 1, 2)).astype(np.float32),
+               "spatial_edges": rng.normal(0, 4, (E, N, 2)).astype(np.float32)}
+        hxs = {"human_node_rnn": rng.normal(0, 0.3, (E, 1, 128)).astype(np.float32),
+               "human_human_edge_rnn": rng.normal(0, 0.3, (E, N + 1, 256)).astype(np.float32)}
+        masks = np.array([[1.0], [0.0], [1.0], [1.0]], np.float32)
+        with torch.no_grad():
+            t_obs = {k: torch.from_numpy(v) for k, v in obs.items()}
+            t_hxs = {k: torch.from_numpy(v.copy()) for k, v in hxs.items()}
+            value, action, logp, nh = pol.act(t_obs, t_hxs, torch.from_numpy(masks), deterministic=True)
+        p = "N%d_" % N
+        for k, v in obs.items():
+            out[p + "act_obs_" + k] = v
+        for k, v in hxs.items():
+            out[p + "act_hxs_" + k] = v
+        out[p + "act_masks"] = masks
+        out[p + "act_value"] = value.numpy()
+        out[p + "act_action"] = action.numpy()
+        out[p + "act_logp"] = logp.numpy()
+        for k, v in nh.items():
+            out[p + "act_new_" + k] = v.numpy()
+        # evaluate_actions (training mode: seq T, nenv E with mid-sequence episode starts)
+        obs_T = {"robot_node": rng.normal(0, 3, (T * E, 1, 7)).astype(np.float32),
+                 "temporal_edges": rng.normal(0, 0.5, (T * E, 1, 2)).astype(np.float32),
+                 "spatial_edges": rng.normal(0, 4, (T * E, N, 2)).astype(np.float32)}
+        hxs0 = {"human_node_rnn": rng.normal(0, 0.3, (E, 1, 128)).astype(np.float32),
+                "human_human_edge_rnn": rng.normal(0, 0.3, (E, N + 1, 256)).astype(np.float32)}
+        masks_T = np.ones((T * E, 1), np.float32)
+        masks_T[3 * E + 1] = 0.0
+        masks_T[5 * E + 2] = 0.0
+        masks_T[0 * E + 0] = 0.0
+        acts = rng.normal(0, 0.5, (T * E, 2)).astype(np.float32)
+        with torch.no_grad():
+            v2, lp2, ent, _ = pol.evaluate_actions({k: torch.from_numpy(v) for k, v in obs_T.items()},
+                                                   {k: torch.from_numpy(v.copy()) for k, v in hxs0.items()},
+                                                   torch.from_numpy(masks_T), torch.from_numpy(acts))
+        for k, v in obs_T.items():
+            out[p + "ev_obs_" + k] = v
+        for k, v in hxs0.items():
+            out[p + "ev_hxs_" + k] = v
+        out[p + "ev_masks"] = masks_T
+        out[p + "ev_actions"] = acts
+        out[p + "ev_value"] = v2.numpy()
+        out[p + "ev_logp"] = lp2.numpy()
+        out[p + "ev_entropy"] = np.array(float(ent))
+        out[p + "keys"] = np.array(sorted(pol.state_dict().keys()))
+        out[p + "shapes"] = np.array([str(tuple(v.shape)) for k, v in sorted(pol.state_dict().items())])
+    np.savez_compressed(os.path.join(outdir, "dsrnn.npz"), **out)
+    print("dsrnn ok")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    os.makedirs(args.out, exist_ok=True)
+    only = set(args.only.split(",")) if args.only else None
+
+    def want(n):
+        return only is None or n in only
+
+    spawn_cases = [
+        ("holo_circle_N5", make_ref_config(N=5), 8),
+        ("holo_circle_N10", make_ref_config(N=10), 8),
+        ("uni_circle_N10", make_ref_config(kin="unicycle", N=10), 8),
+        ("holo_square_N10", make_ref_config(N=10, scenarios=("square_crossing",)), 8),
+        ("holo_parallel_N5", make_ref_config(N=5, scenarios=("parallel_traffic",)), 8),
+        ("holo_perp_N5", make_ref_config(N=5, scenarios=("perpendicular_traffic",)), 8),
+        ("side_pref_N1", make_ref_config(N=1, side_pref=True, scenarios=(
+            "side_pref_passing", "side_pref_overtaking", "side_pref_crossing")), 3),
+        ("uni_square_N12", make_ref_config(kin="unicycle", N=12, scenarios=("square_crossing",)), 6),
+    ]
+    for name, cfg, E in spawn_cases:
+        if want("spawn_" + name):
+            gen_spawn(name, cfg, E, 2, args.out)
+
+    roll_cases = [
+        ("holo_orca_circle_N5", make_ref_config(N=5), 8, 60),
+        ("uni_orca_circle_N10", make_ref_config(kin="unicycle", N=10), 6, 60),
+        ("holo_sf_circle_N5", make_ref_config(policy="social_force", N=5), 6, 60),
+        ("uni_sf_circle_N5", make_ref_config(kin="unicycle", policy="social_force", N=5), 4, 40),
+        ("holo_orca_square_fov_N12", make_ref_config(N=12, scenarios=("square_crossing",), fov_robot=1.0,
+                                                     fov_human=1.0), 4, 40),
+        ("uni_orca_square_fov_N12", make_ref_config(kin="unicycle", N=12, scenarios=("square_crossing",),
+                                                    fov_robot=1.0, fov_human=1.0), 4, 40),
+        ("holo_orca_parallel_N5", make_ref_config(N=5, scenarios=("parallel_traffic",)), 4, 40),
+        ("holo_orca_perp_N5", make_ref_config(N=5, scenarios=("perpendicular_traffic",)), 4, 40),
+        ("holo_orca_sidepref_N1", make_ref_config(N=1, side_pref=True, scenarios=(
+            "side_pref_passing", "side_pref_overtaking", "side_pref_crossing")), 3, 40),
+        ("holo_orca_normzone_N5", make_ref_config(N=5, norm_zones=True), 4, 40),
+        ("holo_orca_visible_N5", make_ref_config(N=5, robot_visible=True, random_radii=True,
+                                                 random_v_pref=True, time_factor=True), 4, 60),
+        ("holo_orca_timeout_N3", make_ref_config(N=3), 2, 200),
+    ]
+    for name, cfg, E, T in roll_cases:
+        if want("roll_" + name):
+            gen_roll(name, cfg, E, T, args.out, goal_frac=0.0 if "timeout" in name else 0.5)
+    if want("dsrnn"):
+        gen_dsrnn(args.out)
+
+
+if __name__ == "__main__":
+    main()

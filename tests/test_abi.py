@@ -1,0 +1,87 @@
+"""C-ABI boundary checks that run without a GPU: the native library loads, exports every symbol
+include/crowdnav.h declares, and agrees with the Python layout mirror (no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from crowdnav_dsrnn_amd import abi, _lib
+from crowdnav_dsrnn_amd.config import Config, UnsupportedConfig, clone_config, make_cn_config
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    txt = open(os.path.join(REPO, "include", "crowdnav.h")).read()
+    return sorted(set(re.findall(r"\b(cn_[a-z_]+)\s*\(", txt)) - {"cn_engine"})
+
+
+@pytest.fixture(scope="module")
+def L():
+    from crowdnav_dsrnn_amd import build
+
+    build.build()
+    return _lib.lib()
+
+
+def test_header_declares_expected_api():
+    assert set(declared_symbols()) == set(_lib.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol(L):
+    for sym in declared_symbols():
+        assert hasattr(L, sym), sym
+
+
+def test_config_struct_size_matches(L):
+    # a validate call on a deliberately invalid config only reads the struct (no GPU work)
+    c = abi.CnConfig()
+    assert L.cn_config_validate(ctypes.byref(c)) != 0
+    assert b"num_envs" in L.cn_last_error()
+
+
+def test_state_layout_matches_python_mirror(L):
+    cfg = make_cn_config(clone_config(Config()), num_envs=37)
+    for N, vis in ((5, 0), (10, 0), (12, 0), (25, 1), (1, 0)):
+        cfg.human_num, cfg.robot_visible = N, vis
+        offs = (ctypes.c_int64 * 64)()
+        tot = ctypes.c_int64()
+        assert L.cn_state_layout_offsets(ctypes.byref(cfg), offs, ctypes.byref(tot)) == 0
+        lay, total = abi.state_layout(37, N, vis)
+        assert total == tot.value
+        for k, (name, _, _) in enumerate(abi.STATE_FIELDS):
+            assert lay[name][0] == offs[k], name
+            nm, tc, ck = ctypes.c_char_p(), ctypes.c_int(), ctypes.c_int()
+            assert L.cn_state_field_info(k, ctypes.byref(nm), ctypes.byref(tc), ctypes.byref(ck)) == 0
+            assert nm.value.decode() == name
+
+
+def test_validate_rejects_unsupported(L):
+    cfg = make_cn_config(clone_config(Config()), num_envs=8)
+    assert L.cn_config_validate(ctypes.byref(cfg)) == 0
+    bad = cfg.copy()
+    bad.human_num = 40
+    assert L.cn_config_validate(ctypes.byref(bad)) != 0
+    bad = cfg.copy()
+    bad.potential_based = 0
+    assert L.cn_config_validate(ctypes.byref(bad)) != 0
+
+
+def test_make_cn_config_rejects_unsupported_reference_options():
+    c = clone_config(Config())
+    c.sim.group_human = True
+    with pytest.raises(UnsupportedConfig):
+        make_cn_config(c, 4)
+    c = clone_config(Config())
+    c.lidar.enable = True
+    with pytest.raises(UnsupportedConfig):
+        make_cn_config(c, 4)
+
+
+def test_make_cn_config_defaults_follow_make_env():
+    c = make_cn_config(clone_config(Config()), num_envs=12)
+    assert c.phase == abi.PHASE_TRAIN and c.nenv == 12   # envs.py:69-73
+    c1 = make_cn_config(clone_config(Config()), num_envs=1)
+    assert c1.phase == abi.PHASE_TEST
+    assert abs(c.robot_fov - 2 * 3.141592653589793) < 1e-12
