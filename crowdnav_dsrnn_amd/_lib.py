@@ -35,7 +35,7 @@ def lib():
     L.cn_destroy.argtypes = [vp]
     L.cn_destroy.restype = None
     L.cn_reset.argtypes = [vp, vp, vp, vp, vp]
-    L.cn_step.argtypes = [vp, vp, vp] + [vp] * 10
+    L.cn_step.argtypes = [vp, vp, vp] + [vp] * 9
     L.cn_state_bytes.argtypes = [vp, ctypes.POINTER(i64)]
     L.cn_state_layout_offsets.argtypes = [cfgp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     L.cn_state_field_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int),
@@ -45,8 +45,12 @@ def lib():
     L.cn_state_device_ptr.argtypes = [vp]
     L.cn_state_device_ptr.restype = vp
     L.cn_edge_features.argtypes = [vp, i64, ctypes.c_int] + [vp] * 14
+    L.cn_profile.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+    L.cn_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(i64)]
     for f in ("cn_config_validate", "cn_create", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
-              "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features"):
+              "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features", "cn_profile",
+              "cn_profile_read"):
         getattr(L, f).restype = i32
     _lib = L
     return L
@@ -60,4 +64,4 @@ def check(rc):
 
 EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "cn_destroy", "cn_reset", "cn_step",
             "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
-            "cn_state_device_ptr", "cn_edge_features"]
+            "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read"]

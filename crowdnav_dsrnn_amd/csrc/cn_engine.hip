@@ -1387,6 +1387,9 @@ struct cn_engine {
     uint32_t *work_count; // [4]
     int64_t case_size, counter_offset;
     int rng_grid;
+    // kernel timing (cn_profile)
+    int prof_on, prof_cap, prof_n;
+    hipEvent_t *ev;  // [3 * prof_cap]: before A, after A, after B
 };
 
 static thread_local char g_err[512];
@@ -1504,10 +1507,51 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     return CN_OK;
 }
 
+static void prof_free(cn_engine *g)
+{
+    if (g->ev) {
+        for (int k = 0; k < 3 * g->prof_cap; ++k) (void)hipEventDestroy(g->ev[k]);
+        delete[] g->ev;
+    }
+    g->ev = nullptr;
+    g->prof_cap = g->prof_n = g->prof_on = 0;
+}
+
+int cn_profile(cn_engine *g, int enable, int max_steps)
+{
+    if (!g) return set_err(CN_EINVAL, "null engine");
+    prof_free(g);
+    if (!enable) return CN_OK;
+    if (max_steps <= 0) return set_err(CN_EINVAL, "max_steps must be > 0");
+    g->ev = new hipEvent_t[3 * max_steps];
+    for (int k = 0; k < 3 * max_steps; ++k) HIPCHK(hipEventCreate(&g->ev[k]));
+    g->prof_cap = max_steps;
+    g->prof_on = 1;
+    return CN_OK;
+}
+
+int cn_profile_read(cn_engine *g, double *a_ms, double *b_ms, int64_t *launches)
+{
+    if (!g) return set_err(CN_EINVAL, "null engine");
+    double sa = 0, sb = 0;
+    if (g->prof_n > 0) HIPCHK(hipEventSynchronize(g->ev[3 * (g->prof_n - 1) + 2]));
+    for (int k = 0; k < g->prof_n; ++k) {
+        float ta = 0, tb = 0;
+        HIPCHK(hipEventElapsedTime(&ta, g->ev[3 * k], g->ev[3 * k + 1]));
+        HIPCHK(hipEventElapsedTime(&tb, g->ev[3 * k + 1], g->ev[3 * k + 2]));
+        sa += ta; sb += tb;
+    }
+    if (a_ms) *a_ms = sa;
+    if (b_ms) *b_ms = sb;
+    if (launches) *launches = g->prof_n;
+    return CN_OK;
+}
+
 void cn_destroy(cn_engine *g)
 {
     if (!g) return;
     hipSetDevice(g->device);
+    prof_free(g);
     hipFree(g->state);
     hipFree(g->work);
     hipFree(g->work_count);
@@ -1533,6 +1577,8 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     if (!g || !actions || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
     HIPCHK(hipMemsetAsync(g->work_count, 0, 16, st));
+    const bool prof = g->prof_on && g->prof_n < g->prof_cap;
+    if (prof) HIPCHK(hipEventRecord(g->ev[3 * g->prof_n], st));
     StepArgs a;
     a.s = g->s; a.actions = actions; a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
     a.reward = reward; a.done = done; a.event = event; a.info = info; a.ep_return = ep_return; a.ep_len = ep_len;
@@ -1540,12 +1586,17 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     const int blocks = (g->E + g->plan.EPB - 1) / g->plan.EPB;
     hipLaunchKernelGGL(cn_step_kernel, dim3(blocks), dim3(CN_BLK), g->plan.total, st, a, g->c);
     HIPCHK(hipGetLastError());
+    if (prof) HIPCHK(hipEventRecord(g->ev[3 * g->prof_n + 1], st));
     RngArgs b;
     b.s = g->s; b.work = g->work; b.work_count = g->work_count; b.reset_all = 0; b.E = g->E;
     b.case_size = g->case_size; b.counter_offset = g->counter_offset;
     b.robot_node = robot_node; b.temporal = temporal; b.spatial = spatial;
     hipLaunchKernelGGL(cn_rng_kernel, dim3(g->rng_grid), dim3(64), 0, st, b, g->c);
     HIPCHK(hipGetLastError());
+    if (prof) {
+        HIPCHK(hipEventRecord(g->ev[3 * g->prof_n + 2], st));
+        ++g->prof_n;
+    }
     return CN_OK;
 }
 

@@ -12,10 +12,13 @@
 
 namespace cn {
 
-__device__ __forceinline__ double dsqrt(double x) { return __dsqrt_rn(x); }
-__device__ __forceinline__ float fsqrt(float x) { return __fsqrt_rn(x); }
-__device__ __forceinline__ double ddiv(double a, double b) { return __ddiv_rn(a, b); }
-__device__ __forceinline__ float fdiv(float a, float b) { return __fdiv_rn(a, b); }
+// IEEE correctly rounded sqrt / division. NOTE: HIP's __fsqrt_rn maps to __ocml_native_sqrt_f32
+// (approximate) unless OCML_BASIC_ROUNDED_OPERATIONS is defined, so the builtins are used: without
+// !fpmath metadata the AMDGPU backend lowers llvm.sqrt.f32/f64 and fdiv to correctly rounded sequences.
+__device__ __forceinline__ double dsqrt(double x) { return __builtin_sqrt(x); }
+__device__ __forceinline__ float fsqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ double ddiv(double a, double b) { return a / b; }
+__device__ __forceinline__ float fdiv(float a, float b) { return a / b; }
 
 // np.linalg.norm of a float64 2-vector: sqrt(fma(b, b, a*a))  (OpenBLAS ddot tail loop is fused)
 __device__ __forceinline__ double np_norm2(double a, double b) { return dsqrt(__fma_rn(b, b, a * a)); }

@@ -159,6 +159,12 @@ int cn_get_state(cn_engine *eng, void *stream, void *dst, int dst_on_host);
 int cn_set_state(cn_engine *eng, void *stream, const void *src, int src_on_host);
 const void *cn_state_device_ptr(const cn_engine *eng);
 
+/* Kernel timing (measurement hook for bench.py's roofline): while enabled, cn_step records HIP events
+ * on its stream around the step kernel (A) and the RNG/auto-reset kernel (B) for up to `max_steps`
+ * calls. cn_profile_read synchronises on the last event and returns the summed kernel times. */
+int cn_profile(cn_engine *eng, int enable, int max_steps);
+int cn_profile_read(cn_engine *eng, double *step_kernel_ms, double *rng_kernel_ms, int64_t *launches);
+
 /* Fused DSRNN edge-feature assembly (SRNN input layers), float32, device pointers.
  *   robot_node [E][7], temporal [E][2], spatial [E][N][2]
  *   Wt [64][2] bt[64]  (humanhumanEdgeRNN_temporal.encoder_linear)

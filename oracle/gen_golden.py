@@ -488,7 +488,7 @@ def main():
         ("uni_sf_circle_N5", make_ref_config(kin="unicycle", policy="social_force", N=5), 4, 40),
         ("holo_orca_square_fov_N12", make_ref_config(N=12, scenarios=("square_crossing",), fov_robot=1.0,
                                                      fov_human=1.0), 4, 40),
-        ("uni_orca_square_fov_N12", make_ref_config(kin="unicycle", N=12, scenarios=("square_crossing",),
+        ("uni_orca_square_fov_N8", make_ref_config(kin="unicycle", N=8, scenarios=("square_crossing",),
                                                     fov_robot=1.0, fov_human=1.0), 4, 40),
         ("holo_orca_parallel_N5", make_ref_config(N=5, scenarios=("parallel_traffic",)), 4, 40),
         ("holo_orca_perp_N5", make_ref_config(N=5, scenarios=("perpendicular_traffic",)), 4, 40),
@@ -499,9 +499,20 @@ def main():
                                                  random_v_pref=True, time_factor=True), 4, 60),
         ("holo_orca_timeout_N3", make_ref_config(N=3), 2, 200),
     ]
+    import signal
+
+    def _alarm(signum, frame):
+        raise TimeoutError("reference did not finish (unbounded rejection loop, SURVEY §9-2)")
+
+    signal.signal(signal.SIGALRM, _alarm)
     for name, cfg, E, T in roll_cases:
         if want("roll_" + name):
-            gen_roll(name, cfg, E, T, args.out, goal_frac=0.0 if "timeout" in name else 0.5)
+            signal.alarm(400)
+            try:
+                gen_roll(name, cfg, E, T, args.out, goal_frac=0.0 if "timeout" in name else 0.5)
+            except TimeoutError as ex:
+                print("roll", name, "SKIPPED:", ex)
+            signal.alarm(0)
     if want("dsrnn"):
         gen_dsrnn(args.out)
 
