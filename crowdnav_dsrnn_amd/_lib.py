@@ -9,7 +9,7 @@ import os
 from . import abi
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libcrowdnav_hip.so")
+LIB_PATH = os.environ.get("CN_LIB_PATH") or os.path.join(HERE, "lib", "libcrowdnav_hip.so")
 
 _lib = None
 

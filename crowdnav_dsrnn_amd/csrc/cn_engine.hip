@@ -1,17 +1,17 @@
 // cn_engine.hip — MI355X (gfx950) batched CrowdSimDict engine: kernels + C ABI (include/crowdnav.h).
 //
 // Hot path per cn_step (one HIP stream, no host synchronisation):
-//   1. hipMemsetAsync(work_count)            — per-step RNG worklist reset (4 bytes)
-//   2. cn_step_kernel   (kernel A)           — one lane per (env, human), 256-lane workgroups holding
+//   1. cn_step_kernel   (kernel A)           — one lane per (env, human), 256-lane workgroups holding
 //                                              floor(256/N) whole envs: SRNN.clip_action, the human
 //                                              policies (ORCA LP / social force) on the PRE-move state,
 //                                              calc_reward, kinematics, observation, Monitor; envs that
 //                                              need random numbers (reset, goal changes) are appended
 //                                              to a device worklist.
-//   3. cn_rng_kernel    (kernel B)           — one wave per listed env: numpy-legacy MT19937 in LDS,
+//   2. cn_rng_kernel    (kernel B)           — one wave per listed env: numpy-legacy MT19937 in LDS,
 //                                              update_human_goals_randomly / update_human_goal, and the
 //                                              VecEnv auto-reset (CrowdSimDict.reset: reseed + spawn +
-//                                              first observation).
+//                                              first observation). Worklist counters are double
+//                                              buffered: kernel B zeroes the next step's counter.
 // Reference: crowd_sim/envs/crowd_sim_dict.py:105-271, crowd_sim/envs/crowd_sim.py:296-1161,
 // crowd_sim/envs/utils/agent.py:172-218, crowd_nav/policy/{orca,social_force,srnn}.py; RVO2 v2.0
 // (third-party) restated in float32. Numerics: see cn_math.h.
@@ -27,6 +27,19 @@
 using namespace cn;
 
 #define CN_BLK 256
+
+// Diagnostic build only (-DCN_STAMPS): per-workgroup s_memtime stamps at phase boundaries, read back
+// with cn_debug_stamps(). The shipped library is built without it (no stamp executes).
+#ifdef CN_STAMPS
+#define CN_NSTAMP 8
+__device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
+__device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
+#define STAMP_A(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + (k)] = clock64(); } while (0)
+#define STAMP_B(w, k) do { if (threadIdx.x == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
+#else
+#define STAMP_A(k) do { } while (0)
+#define STAMP_B(w, k) do { } while (0)
+#endif
 #define CN_MAX_A 32
 #define CN_DUMMY_POS 7.0
 
@@ -34,12 +47,13 @@ using namespace cn;
 // launch geometry + LDS plan of kernel A
 // ------------------------------------------------------------------------------------------------
 struct StepPlan {
+    int T;       // threads per workgroup (256; 128 when N > 12 so the kd-tree path's LDS lines fit)
     int EPB;     // envs per workgroup
     int M;       // observed slots per human (ORCA lines upper bound)
     int A;       // agents per RVO2 simulator
     int kd;      // A > 10: KdTree ordering needed
     // LDS byte offsets
-    int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_lines, o_nd, o_ns, o_perm, total;
+    int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_lines, o_proj, o_nd, o_ns, o_perm, total;
 };
 
 #define CN_RENV_F 14   // robot/env doubles per env in LDS
@@ -50,11 +64,13 @@ __host__ __device__ inline int cn_align16(int x) { return (x + 15) & ~15; }
 __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
 {
     StepPlan p;
-    p.EPB = CN_BLK / N;
     p.A = N + (robot_visible ? 1 : 0);
     p.M = p.A - 1;
     p.kd = p.A > 10;
-    const int T = CN_BLK;
+    p.T = N > 12 ? 128 : CN_BLK;
+    p.EPB = p.T / N;
+    const int T = p.T;
+    const int ML = p.kd ? (p.M > 0 ? p.M : 1) : 0;   // LDS ORCA lines only on the kd-tree path
     int o = 0;
     p.o_renv = o;  o = cn_align16(o + CN_RENV_F * p.EPB * 8);
     p.o_racts = o; o = cn_align16(o + 2 * p.EPB * 4);
@@ -63,9 +79,10 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_hum = o;   o = cn_align16(o + CN_HUM_F * T * 8);
     p.o_lane = o;  o = cn_align16(o + T * 8 + T * 4);      // closest distance (f64) + flag word
     p.o_orad = o;  o = cn_align16(o + T * 4);
-    p.o_lines = o; o = cn_align16(o + (p.M > 0 ? p.M : 1) * T * 16);
-    p.o_nd = o;    o = cn_align16(o + (p.M > 0 ? p.M : 1) * T * 4);
-    p.o_ns = o;    o = cn_align16(o + (p.M > 0 ? p.M : 1) * T);
+    p.o_lines = o; o = cn_align16(o + ML * T * 16);
+    p.o_proj = o;  o = cn_align16(o + ML * T * 16);
+    p.o_nd = o;    o = cn_align16(o + ML * T * 4);
+    p.o_ns = o;    o = cn_align16(o + ML * T);
     p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * T : 0));
     p.total = o;
     return p;
@@ -73,6 +90,7 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
 
 // kernel-A LDS views
 struct SL {
+    int T;            // lane stride of the per-lane arrays
     double *r;        // [CN_RENV_F][EPB]
     float *act;       // [2][EPB] clipped action (holonomic vx,vy / unicycle v,r)
     uint32_t *rflag;  // [EPB] flags ; [EPB] aux
@@ -81,7 +99,8 @@ struct SL {
     double *cd;       // [T]
     uint32_t *lf;     // [T]
     float *orad;      // [T]
-    float4 *lines;    // [M][T]
+    float4 *lines;    // [M][T]  (kd-tree path)
+    float4 *proj;     // [M][T]  linearProgram3's projected lines (kd-tree path)
     float *nd;        // [M][T]
     uint8_t *ns;      // [M][T]
     uint8_t *perm;    // [A][T]
@@ -89,7 +108,7 @@ struct SL {
 enum { R_PX, R_PY, R_GX, R_GY, R_VX, R_VY, R_TH, R_RAD, R_VP, R_POT, R_GT, R_DV, R_NX, R_NY };
 enum { H_PX, H_PY, H_GX, H_GY, H_VX, H_VY, H_R, H_VP, H_TH };
 #define RF(sl, f, el, EPB) ((sl).r[(f) * (EPB) + (el)])
-#define HF(sl, f, t) ((sl).h[(f) * CN_BLK + (t)])
+#define HF(sl, f, t) ((sl).h[(f) * (sl).T + (t)])
 
 // lane flag bits
 #define LF_VR 1u
@@ -230,18 +249,19 @@ __constant__ double c_circ_sin[64];
 
 __device__ inline bool disc_quad_intersect(double px, double py, double r, const double *qx, const double *qy)
 {
-    double vx[64], vy[64];
-    for (int k = 0; k < 64; ++k) { vx[k] = px + r * c_circ_cos[k]; vy[k] = py + r * c_circ_sin[k]; }
-    vx[0] = px + r; vy[0] = py;
+    // vertices recomputed on the fly (no 64-entry arrays: keeps the step kernel's VGPR budget)
+    auto VX = [&](int k) { return k == 0 ? px + r : px + r * c_circ_cos[k]; };
+    auto VY = [&](int k) { return k == 0 ? py : py + r * c_circ_sin[k]; };
     for (int p = 0; p < 2; ++p) {
         const int nv = p ? 64 : 4;
-        const double *ex_ = p ? vx : qx, *ey_ = p ? vy : qy;
         for (int k = 0; k < nv; ++k) {
-            const double ex = ex_[(k + 1) % nv] - ex_[k], ey = ey_[(k + 1) % nv] - ey_[k];
+            const int k1 = (k + 1) % nv;
+            const double ex = p ? VX(k1) - VX(k) : qx[k1] - qx[k];
+            const double ey = p ? VY(k1) - VY(k) : qy[k1] - qy[k];
             if (ex == 0.0 && ey == 0.0) continue;
             const double nx = -ey, ny = ex;
             double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
-            for (int v = 0; v < 64; ++v) { const double t = vx[v] * nx + vy[v] * ny; amin = t < amin ? t : amin; amax = t > amax ? t : amax; }
+            for (int v = 0; v < 64; ++v) { const double t = VX(v) * nx + VY(v) * ny; amin = t < amin ? t : amin; amax = t > amax ? t : amax; }
             for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
             if (amax < bmin || bmax < amin) return false;
         }
@@ -256,9 +276,9 @@ __device__ inline bool disc_quad_intersect(double px, double py, double r, const
 
 struct LineView {
     float4 *base;
-    int tid;
-    __device__ float4 operator[](int k) const { return base[k * CN_BLK + tid]; }
-    __device__ void set(int k, float4 v) const { base[k * CN_BLK + tid] = v; }
+    int tid, T;
+    __device__ float4 operator[](int k) const { return base[k * T + tid]; }
+    __device__ void set(int k, float4 v) const { base[k * T + tid] = v; }
 };
 
 __device__ inline float det2(float ax, float ay, float bx, float by) { return ax * by - ay * bx; }
@@ -297,9 +317,10 @@ __device__ bool lp1(const LineView &L, int no, float radius, float ox, float oy,
     return true;
 }
 
-__device__ int lp2(const LineView &L, int n, float radius, float ox, float oy, float &rx, float &ry)
+__device__ int lp2(const LineView &L, int n, float radius, float ox, float oy, float &rx, float &ry, bool dirOpt = false)
 {
-    if (ox * ox + oy * oy > radius * radius) {
+    if (dirOpt) { rx = ox * radius; ry = oy * radius; }
+    else if (ox * ox + oy * oy > radius * radius) {
         const float inv = fdiv(1.0f, fsqrt(ox * ox + oy * oy));
         rx = (ox * inv) * radius; ry = (oy * inv) * radius;
     } else { rx = ox; ry = oy; }
@@ -307,16 +328,16 @@ __device__ int lp2(const LineView &L, int n, float radius, float ox, float oy, f
         const float4 li = L[i];
         if (det2(li.z, li.w, li.x - rx, li.y - ry) > 0.0f) {
             const float tx = rx, ty = ry;
-            if (!lp1(L, i, radius, ox, oy, false, rx, ry)) { rx = tx; ry = ty; return i; }
+            if (!lp1(L, i, radius, ox, oy, dirOpt, rx, ry)) { rx = tx; ry = ty; return i; }
         }
     }
     return n;
 }
 
-// projected line j of LP3's line i (recomputed on the fly; `valid` false when skipped)
-__device__ inline float4 proj_line(const float4 li, const float4 lj, bool &valid)
+// projected line of LP3's line li against lj (`valid` false when RVO2 skips it: parallel, same direction)
+__device__ __forceinline__ float4 proj_line(const float4 li, const float4 lj, bool &valid)
 {
-    float4 r;
+    float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
     const float determinant = det2(li.z, li.w, lj.z, lj.w);
     valid = true;
     if (fabsf(determinant) <= RVO_EPSILON) {
@@ -334,61 +355,193 @@ __device__ inline float4 proj_line(const float4 li, const float4 lj, bool &valid
     return r;
 }
 
-// linearProgram1 (direction-optimal) over the projected lines of line `li` (lines < ii)
-__device__ bool lp1_proj(const LineView &L, int ii, int no, float radius, float ox, float oy, float &rx, float &ry)
-{
-    const float4 li = L[ii];
-    bool v;
-    const float4 ln = proj_line(li, L[no], v);
-    const float dot = ln.x * ln.z + ln.y * ln.w;
-    const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
-    if (disc < 0.0f) return false;
-    const float sd = fsqrt(disc);
-    float tL = -dot - sd, tR = -dot + sd;
-    for (int i = 0; i < no; ++i) {
-        bool vi;
-        const float4 pi = proj_line(li, L[i], vi);
-        if (!vi) continue;
-        const float den = det2(ln.z, ln.w, pi.z, pi.w);
-        const float num = det2(pi.z, pi.w, ln.x - pi.x, ln.y - pi.y);
-        if (fabsf(den) <= RVO_EPSILON) {
-            if (num < 0.0f) return false;
-            continue;
-        }
-        const float t = fdiv(num, den);
-        if (den >= 0.0f) tR = (t < tR) ? t : tR;
-        else tL = (tL < t) ? t : tL;
-        if (tL > tR) return false;
-    }
-    if (ox * ln.z + oy * ln.w > 0.0f) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
-    else { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
-    return true;
-}
-
-__device__ void lp3(const LineView &L, int n, int begin, float radius, float &rx, float &ry)
+// linearProgram3 (numObstLines = 0); projected lines stored once per violating line in `PL`
+__device__ void lp3(const LineView &L, const LineView &PL, int n, int begin, float radius, float &rx, float &ry)
 {
     float distance = 0.0f;
     for (int i = begin; i < n; ++i) {
         const float4 li = L[i];
         if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
-            const float tx = rx, ty = ry;
-            // linearProgram2(projLines, radius, (-dir_i.y, dir_i.x), directionOpt = true)
-            const float ox = -li.w, oy = li.z;
-            rx = ox * radius; ry = oy * radius;
-            bool fail = false;
-            for (int j = 0; j < i && !fail; ++j) {
-                bool vj;
-                const float4 pj = proj_line(li, L[j], vj);
-                if (!vj) continue;
-                if (det2(pj.z, pj.w, pj.x - rx, pj.y - ry) > 0.0f) {
-                    const float sx = rx, sy = ry;
-                    if (!lp1_proj(L, i, j, radius, ox, oy, rx, ry)) { rx = sx; ry = sy; fail = true; }
-                }
+            int np = 0;
+            for (int j = 0; j < i; ++j) {
+                bool v;
+                const float4 pj = proj_line(li, L[j], v);
+                if (v) PL.set(np++, pj);
             }
-            if (fail) { rx = tx; ry = ty; }
+            const float tx = rx, ty = ry;
+            if (lp2(PL, np, radius, -li.w, li.z, rx, ry, true) < np) { rx = tx; ry = ty; }
             distance = det2(li.z, li.w, li.x - rx, li.y - ry);
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// register-resident RVO2 for simulators of <= 10 agents (<= 9 ORCA lines): every line index is a
+// compile-time constant after full unrolling, so lines / projected lines live in VGPRs
+// ------------------------------------------------------------------------------------------------
+#define RMM 9
+
+// linearProgram1, branch-free over the earlier lines: RVO2 exits as soon as tLeft > tRight or a
+// parallel line has numerator < 0; tLeft only grows and tRight only shrinks, so "exit at some prefix"
+// equals "tLeft > tRight at the end", and the parallel-line test is order independent. Evaluating all
+// lines first gives the same result while the divisions are independent (ILP).
+__device__ __forceinline__ bool lp1_core(const float4 ln, const float4 (&L)[RMM], const bool (&V)[RMM], const int no,
+                                         bool useV, float radius, float &tL, float &tR)
+{
+    const float dot = ln.x * ln.z + ln.y * ln.w;
+    const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
+    bool fail = disc < 0.0f;
+    const float sd = fsqrt(disc);
+    tL = -dot - sd;
+    tR = -dot + sd;
+#pragma unroll
+    for (int i = 0; i < RMM; ++i) {
+        if (i < no && (!useV || V[i])) {
+            const float4 li = L[i];
+            const float den = det2(ln.z, ln.w, li.z, li.w);
+            const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
+            const bool par = fabsf(den) <= RVO_EPSILON;
+            fail = fail || (par && num < 0.0f);
+            const float t = fdiv(num, den);
+            tR = (!par && den >= 0.0f && t < tR) ? t : tR;
+            tL = (!par && !(den >= 0.0f) && tL < t) ? t : tL;
+        }
+    }
+    return !(fail || tL > tR);
+}
+
+__device__ __forceinline__ bool lp1_r(const float4 (&L)[RMM], const int no, float radius, float ox, float oy,
+                                      bool dirOpt, float &rx, float &ry)
+{
+    const float4 ln = L[no];
+    float tL, tR;
+    const bool V[RMM] = {};
+    if (!lp1_core(ln, L, V, no, false, radius, tL, tR)) return false;
+    if (dirOpt) {
+        if (ox * ln.z + oy * ln.w > 0.0f) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
+        else { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
+    } else {
+        const float t = ln.z * (ox - ln.x) + ln.w * (oy - ln.y);
+        if (t < tL) { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
+        else if (t > tR) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
+        else { rx = ln.x + t * ln.z; ry = ln.y + t * ln.w; }
+    }
+    return true;
+}
+
+// linearProgram1 (direction-optimal) over projected lines with RVO2's skipped ones marked invalid
+__device__ __forceinline__ bool lp1p_r(const float4 (&P)[RMM], const bool (&V)[RMM], const int no, float radius,
+                                       float ox, float oy, float &rx, float &ry)
+{
+    const float4 ln = P[no];
+    float tL, tR;
+    if (!lp1_core(ln, P, V, no, true, radius, tL, tR)) return false;
+    if (ox * ln.z + oy * ln.w > 0.0f) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
+    else { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
+    return true;
+}
+
+__device__ __forceinline__ int lp2_r(const float4 (&L)[RMM], int n, float radius, float ox, float oy, float &rx,
+                                     float &ry)
+{
+    if (ox * ox + oy * oy > radius * radius) {
+        const float inv = fdiv(1.0f, fsqrt(ox * ox + oy * oy));
+        rx = (ox * inv) * radius; ry = (oy * inv) * radius;
+    } else { rx = ox; ry = oy; }
+#pragma unroll
+    for (int i = 0; i < RMM; ++i) {
+        if (i < n) {
+            const float4 li = L[i];
+            if (det2(li.z, li.w, li.x - rx, li.y - ry) > 0.0f) {
+                const float tx = rx, ty = ry;
+                if (!lp1_r(L, i, radius, ox, oy, false, rx, ry)) { rx = tx; ry = ty; return i; }
+            }
+        }
+    }
+    return n;
+}
+
+__device__ __forceinline__ void lp3_r(const float4 (&L)[RMM], int n, int begin, float radius, float &rx, float &ry)
+{
+    float distance = 0.0f;
+#pragma unroll
+    for (int i = 0; i < RMM; ++i) {
+        if (i >= begin && i < n) {
+            const float4 li = L[i];
+            if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
+                float4 P[RMM];
+                bool V[RMM];
+#pragma unroll
+                for (int j = 0; j < RMM; ++j) {
+                    V[j] = false;
+                    P[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (j < i) P[j] = proj_line(li, L[j], V[j]);
+                }
+                const float tx = rx, ty = ry;
+                const float ox = -li.w, oy = li.z;   // linearProgram2(projLines, radius, (-d.y, d.x), true)
+                rx = ox * radius; ry = oy * radius;
+                bool fail = false;
+#pragma unroll
+                for (int k = 0; k < RMM; ++k) {
+                    if (k < i && V[k] && !fail) {
+                        const float4 pk = P[k];
+                        if (det2(pk.z, pk.w, pk.x - rx, pk.y - ry) > 0.0f) {
+                            const float sx = rx, sy = ry;
+                            if (!lp1p_r(P, V, k, radius, ox, oy, rx, ry)) { rx = sx; ry = sy; fail = true; }
+                        }
+                    }
+                }
+                if (fail) { rx = tx; ry = ty; }
+                distance = det2(li.z, li.w, li.x - rx, li.y - ry);
+            }
+        }
+    }
+}
+
+// one ORCA line (Agent::computeNewVelocity, agent branch) of self vs another agent
+__device__ __forceinline__ float4 orca_line(float X0, float Y0, float VX0, float VY0, float R0, float ox, float oy,
+                                           float ovx, float ovy, float orr, float invTH, float invTS)
+{
+    const float rpx = ox - X0, rpy = oy - Y0;
+    const float rvx = VX0 - ovx, rvy = VY0 - ovy;
+    const float distSq = rpx * rpx + rpy * rpy;
+    const float cr = R0 + orr;
+    const float crSq = cr * cr;
+    float ux, uy, dx, dy;
+    if (distSq > crSq) {
+        const float wx = rvx - invTH * rpx, wy = rvy - invTH * rpy;
+        const float wLenSq = wx * wx + wy * wy;
+        const float dot1 = wx * rpx + wy * rpy;
+        if (dot1 < 0.0f && dot1 * dot1 > crSq * wLenSq) {
+            const float wLen = fsqrt(wLenSq);
+            const float inv = fdiv(1.0f, wLen);
+            const float uwx = wx * inv, uwy = wy * inv;
+            dx = uwy; dy = -uwx;
+            const float s = cr * invTH - wLen;
+            ux = s * uwx; uy = s * uwy;
+        } else {
+            const float leg = fsqrt(distSq - crSq);
+            const float inv = fdiv(1.0f, distSq);
+            if (det2(rpx, rpy, wx, wy) > 0.0f) {
+                dx = (rpx * leg - rpy * cr) * inv;
+                dy = (rpx * cr + rpy * leg) * inv;
+            } else {
+                dx = -((rpx * leg + rpy * cr) * inv);
+                dy = -((-rpx * cr + rpy * leg) * inv);
+            }
+            const float dot2 = rvx * dx + rvy * dy;
+            ux = dot2 * dx - rvx; uy = dot2 * dy - rvy;
+        }
+    } else {
+        const float wx = rvx - invTS * rpx, wy = rvy - invTS * rpy;
+        const float wLen = fsqrt(wx * wx + wy * wy);
+        const float inv = fdiv(1.0f, wLen);
+        const float uwx = wx * inv, uwy = wy * inv;
+        dx = uwy; dy = -uwx;
+        const float s = cr * invTS - wLen;
+        ux = s * uwx; uy = s * uwy;
+    }
+    return make_float4(VX0 + 0.5f * ux, VY0 + 0.5f * uy, dx, dy);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -405,7 +558,7 @@ struct StepArgs {
     double *ep_return;
     int32_t *ep_len;
     uint32_t *work;
-    uint32_t *work_count;
+    uint32_t *work_count;   // this step's counter (work_counts[step & 1])
     int E;
 };
 
@@ -439,14 +592,15 @@ __device__ inline void insert_nbr(const SL &sl, int tid, int &cnt, int maxN, int
     if (distSq < rangeSq) {
         if (cnt < maxN) ++cnt;
         int q = cnt - 1;
-        while (q != 0 && distSq < sl.nd[(q - 1) * CN_BLK + tid]) {
-            sl.nd[q * CN_BLK + tid] = sl.nd[(q - 1) * CN_BLK + tid];
-            sl.ns[q * CN_BLK + tid] = sl.ns[(q - 1) * CN_BLK + tid];
+        const int T = sl.T;
+        while (q != 0 && distSq < sl.nd[(q - 1) * T + tid]) {
+            sl.nd[q * T + tid] = sl.nd[(q - 1) * T + tid];
+            sl.ns[q * T + tid] = sl.ns[(q - 1) * T + tid];
             --q;
         }
-        sl.nd[q * CN_BLK + tid] = distSq;
-        sl.ns[q * CN_BLK + tid] = (uint8_t)slot;
-        if (cnt == maxN) rangeSq = sl.nd[(cnt - 1) * CN_BLK + tid];
+        sl.nd[q * T + tid] = distSq;
+        sl.ns[q * T + tid] = (uint8_t)slot;
+        if (cnt == maxN) rangeSq = sl.nd[(cnt - 1) * T + tid];
     }
 }
 
@@ -457,6 +611,7 @@ __device__ inline float bbox_dist(float x, float y, float mnx, float mxx, float 
     return a * a + b * b + cc * cc + d * d;
 }
 
+template <bool KD>
 __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -464,15 +619,17 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
     const StepPlan P = cn_step_plan(N, c.robot_visible);
     const int EPB = P.EPB, M = P.M, A = P.A;
     SL sl;
+    sl.T = P.T;
     sl.r = (double *)(smem + P.o_renv);
     sl.act = (float *)(smem + P.o_racts);
     sl.rflag = (uint32_t *)(smem + P.o_rflag);
     sl.rvr = (double *)(smem + P.o_rvr);
     sl.h = (double *)(smem + P.o_hum);
     sl.cd = (double *)(smem + P.o_lane);
-    sl.lf = (uint32_t *)(smem + P.o_lane + CN_BLK * 8);
+    sl.lf = (uint32_t *)(smem + P.o_lane + P.T * 8);
     sl.orad = (float *)(smem + P.o_orad);
     sl.lines = (float4 *)(smem + P.o_lines);
+    sl.proj = (float4 *)(smem + P.o_proj);
     sl.nd = (float *)(smem + P.o_nd);
     sl.ns = (uint8_t *)(smem + P.o_ns);
     sl.perm = (uint8_t *)(smem + P.o_perm);
@@ -489,6 +646,7 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
     const bool holo = c.kinematics == CN_HOLONOMIC;
     const double dt = c.time_step;
 
+    STAMP_A(0);
     // ---- phase 0: load state into LDS -----------------------------------------------------------
     double bpx = 0, bpy = 0, bvx = 0, bvy = 0, br = 0;
     if (hl) {
@@ -531,6 +689,7 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         for (int k = 0; k < 4; ++k) { sl.rvr[k * EPB + tid] = cx[k]; sl.rvr[(4 + k) * EPB + tid] = cy[k]; }
     }
     __syncthreads();
+    STAMP_A(1);
 
     // ---- phase 1: visibility of the other agents to human i, frozen simulator parameters --------
     const bool orca = c.human_policy == CN_POLICY_ORCA;
@@ -566,6 +725,7 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         }
     }
     __syncthreads();
+    STAMP_A(2);
 
     // ---- phase 2: human policy (PRE-move state) + per-human reward terms -------------------------
     double nvx = 0.0, nvy = 0.0;
@@ -578,185 +738,180 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
             const float rdummy = (float)(c.human_radius + 0.01 + c.orca_safety_space);
             const float X0 = (float)px, Y0 = (float)py, VX0 = (float)vx0, VY0 = (float)vy0;
             const float R0 = sl.orad[tid];
-            float rangeSq = (float)c.orca_neighbor_dist * (float)c.orca_neighbor_dist;
-            int cnt = 0;
-            const int maxN = M;
-            if (maxN > 0) {
-                if (!P.kd) {
-                    for (int k = 0; k < M; ++k) {
-                        float x, y, vx, vy, r;
-                        slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, x, y, vx, vy, r);
-                        const float dx = X0 - x, dy = Y0 - y;
-                        insert_nbr(sl, tid, cnt, maxN, k, dx * dx + dy * dy, rangeSq);
-                    }
-                } else {
-                    // KdTree: persisted agents_ order (identity at simulator creation)
-                    uint8_t *perm = sl.perm;
-                    for (int a = 0; a < A; ++a)
-                        perm[a * CN_BLK + tid] = frozen ? S.o_perm[gh * A + a] : (uint8_t)a;
-                    auto AX = [&](int a) -> float {
-                        if (a == 0) return X0;
-                        float x, y, vx, vy, r;
-                        slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
-                        return x;
-                    };
-                    auto AY = [&](int a) -> float {
-                        if (a == 0) return Y0;
-                        float x, y, vx, vy, r;
-                        slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
-                        return y;
-                    };
-                    // build (buildAgentTreeRecursive), iteratively; partitions perm in place
-                    int stb[CN_MAX_A], ste[CN_MAX_A], sp = 0;
-                    stb[sp] = 0; ste[sp] = A; ++sp;
-                    while (sp > 0) {
-                        --sp;
-                        const int b = stb[sp], e = ste[sp];
-                        if (e - b <= 10) continue;
-                        float mnx = AX(perm[b * CN_BLK + tid]), mxx = mnx;
-                        float mny = AY(perm[b * CN_BLK + tid]), mxy = mny;
-                        for (int q = b + 1; q < e; ++q) {
-                            const int a = perm[q * CN_BLK + tid];
-                            const float x = AX(a), y = AY(a);
-                            mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
-                            mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
-                        }
-                        const bool vert = (mxx - mnx > mxy - mny);
-                        const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
-                        int left = b, right = e;
-                        while (left < right) {
-                            while (left < right) {
-                                const int a = perm[left * CN_BLK + tid];
-                                if (!((vert ? AX(a) : AY(a)) < split)) break;
-                                ++left;
-                            }
-                            while (right > left) {
-                                const int a = perm[(right - 1) * CN_BLK + tid];
-                                if (!((vert ? AX(a) : AY(a)) >= split)) break;
-                                --right;
-                            }
-                            if (left < right) {
-                                const uint8_t t0 = perm[left * CN_BLK + tid];
-                                perm[left * CN_BLK + tid] = perm[(right - 1) * CN_BLK + tid];
-                                perm[(right - 1) * CN_BLK + tid] = t0;
-                                ++left; --right;
-                            }
-                        }
-                        if (left == b) { ++left; }
-                        stb[sp] = b; ste[sp] = left; ++sp;
-                        stb[sp] = left; ste[sp] = e; ++sp;
-                    }
-                    for (int a = 0; a < A; ++a) S.o_perm[gh * A + a] = perm[a * CN_BLK + tid];
-                    // query (queryAgentTreeRecursive): closer child first, ties -> right; subtree
-                    // pruning never drops an in-range agent, so visiting every leaf is equivalent
-                    sp = 0; stb[sp] = 0; ste[sp] = A; ++sp;
-                    while (sp > 0) {
-                        --sp;
-                        const int b = stb[sp], e = ste[sp];
-                        if (e - b <= 10) {
-                            for (int q = b; q < e; ++q) {
-                                const int a = perm[q * CN_BLK + tid];
-                                if (a == 0) continue;
-                                const float dx = X0 - AX(a), dy = Y0 - AY(a);
-                                insert_nbr(sl, tid, cnt, maxN, a - 1, dx * dx + dy * dy, rangeSq);
-                            }
-                            continue;
-                        }
-                        float mnx = AX(perm[b * CN_BLK + tid]), mxx = mnx;
-                        float mny = AY(perm[b * CN_BLK + tid]), mxy = mny;
-                        for (int q = b + 1; q < e; ++q) {
-                            const int a = perm[q * CN_BLK + tid];
-                            const float x = AX(a), y = AY(a);
-                            mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
-                            mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
-                        }
-                        const bool vert = (mxx - mnx > mxy - mny);
-                        const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
-                        int left = b;
-                        for (int q = b; q < e; ++q) {
-                            const int a = perm[q * CN_BLK + tid];
-                            if ((vert ? AX(a) : AY(a)) < split) ++left;
-                        }
-                        if (left == b) ++left;
-                        float bb[2][4];
-                        for (int ch = 0; ch < 2; ++ch) {
-                            const int cb = ch ? left : b, ce = ch ? e : left;
-                            float a0x = AX(perm[cb * CN_BLK + tid]), a1x = a0x;
-                            float a0y = AY(perm[cb * CN_BLK + tid]), a1y = a0y;
-                            for (int q = cb + 1; q < ce; ++q) {
-                                const int a = perm[q * CN_BLK + tid];
-                                const float x = AX(a), y = AY(a);
-                                a1x = a1x < x ? x : a1x; a0x = x < a0x ? x : a0x;
-                                a1y = a1y < y ? y : a1y; a0y = y < a0y ? y : a0y;
-                            }
-                            bb[ch][0] = a0x; bb[ch][1] = a1x; bb[ch][2] = a0y; bb[ch][3] = a1y;
-                        }
-                        const float dl = bbox_dist(X0, Y0, bb[0][0], bb[0][1], bb[0][2], bb[0][3]);
-                        const float dr = bbox_dist(X0, Y0, bb[1][0], bb[1][1], bb[1][2], bb[1][3]);
-                        if (dl < dr) {  // visit left first: push right, then left
-                            stb[sp] = left; ste[sp] = e; ++sp; stb[sp] = b; ste[sp] = left; ++sp;
-                        } else {
-                            stb[sp] = b; ste[sp] = left; ++sp; stb[sp] = left; ste[sp] = e; ++sp;
-                        }
-                    }
-                }
-            }
-            // ORCA lines (Agent::computeNewVelocity, agents only)
-            LineView L{sl.lines, tid};
+            const float rangeSq = (float)c.orca_neighbor_dist * (float)c.orca_neighbor_dist;
             const float invTH = fdiv(1.0f, (float)c.orca_time_horizon);
-            for (int p = 0; p < cnt; ++p) {
-                const int k = sl.ns[p * CN_BLK + tid];
-                float ox, oy, ovx, ovy, orr;
-                slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, ox, oy, ovx, ovy, orr);
-                const float rpx = ox - X0, rpy = oy - Y0;
-                const float rvx = VX0 - ovx, rvy = VY0 - ovy;
-                const float distSq = rpx * rpx + rpy * rpy;
-                const float cr = R0 + orr;
-                const float crSq = cr * cr;
-                float ux, uy, dx, dy;
-                if (distSq > crSq) {
-                    const float wx = rvx - invTH * rpx, wy = rvy - invTH * rpy;
-                    const float wLenSq = wx * wx + wy * wy;
-                    const float dot1 = wx * rpx + wy * rpy;
-                    if (dot1 < 0.0f && dot1 * dot1 > crSq * wLenSq) {
-                        const float wLen = fsqrt(wLenSq);
-                        const float inv = fdiv(1.0f, wLen);
-                        const float uwx = wx * inv, uwy = wy * inv;
-                        dx = uwy; dy = -uwx;
-                        const float s = cr * invTH - wLen;
-                        ux = s * uwx; uy = s * uwy;
-                    } else {
-                        const float leg = fsqrt(distSq - crSq);
-                        const float inv = fdiv(1.0f, distSq);
-                        if (det2(rpx, rpy, wx, wy) > 0.0f) {
-                            dx = (rpx * leg - rpy * cr) * inv;
-                            dy = (rpx * cr + rpy * leg) * inv;
-                        } else {
-                            dx = -((rpx * leg + rpy * cr) * inv);
-                            dy = -((-rpx * cr + rpy * leg) * inv);
-                        }
-                        const float dot2 = rvx * dx + rvy * dy;
-                        ux = dot2 * dx - rvx; uy = dot2 * dy - rvy;
-                    }
-                } else {
-                    const float invTS = fdiv(1.0f, (float)dt);
-                    const float wx = rvx - invTS * rpx, wy = rvy - invTS * rpy;
-                    const float wLen = fsqrt(wx * wx + wy * wy);
-                    const float inv = fdiv(1.0f, wLen);
-                    const float uwx = wx * inv, uwy = wy * inv;
-                    dx = uwy; dy = -uwx;
-                    const float s = cr * invTS - wLen;
-                    ux = s * uwx; uy = s * uwy;
-                }
-                L.set(p, make_float4(VX0 + 0.5f * ux, VY0 + 0.5f * uy, dx, dy));
-            }
+            const float invTS = fdiv(1.0f, (float)dt);
             // preferred velocity: unit vector to the goal only if farther than 1 (orca.py:118-122)
             double gdx = HF(sl, H_GX, tid) - px, gdy = HF(sl, H_GY, tid) - py;
             const double speed = np_norm2(gdx, gdy);
             if (speed > 1.0) { gdx = ddiv(gdx, speed); gdy = ddiv(gdy, speed); }
             float rx, ry;
-            const int fail_at = lp2(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
-            if (fail_at < cnt) lp3(L, cnt, fail_at, my_vmax, rx, ry);
+            if constexpr (!KD) {
+                // <= 10 agents: the KdTree is one leaf, so the neighbour list is the in-range slots
+                // stably sorted by distSq (Agent::insertAgentNeighbor); lines and sort in registers
+                float4 raw[RMM], L[RMM];
+                float d[RMM];
+                bool inr[RMM];
+#pragma unroll
+                for (int k = 0; k < RMM; ++k) {
+                    inr[k] = false; d[k] = 0.0f;
+                    raw[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (k < M) {
+                        float x, y, vx, vy, r;
+                        slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, x, y, vx, vy, r);
+                        const float dx = X0 - x, dy = Y0 - y;
+                        d[k] = dx * dx + dy * dy;
+                        inr[k] = d[k] < rangeSq;
+                        raw[k] = orca_line(X0, Y0, VX0, VY0, R0, x, y, vx, vy, r, invTH, invTS);
+                    }
+                }
+                int cnt = 0;
+#pragma unroll
+                for (int k = 0; k < RMM; ++k) { cnt += inr[k] ? 1 : 0; L[k] = make_float4(0.f, 0.f, 0.f, 0.f); }
+#pragma unroll
+                for (int k = 0; k < RMM; ++k) {
+                    int rank = 0;
+#pragma unroll
+                    for (int q = 0; q < RMM; ++q)
+                        rank += (inr[q] && (d[q] < d[k] || (d[q] == d[k] && q < k))) ? 1 : 0;
+#pragma unroll
+                    for (int pp = 0; pp < RMM; ++pp)
+                        if (inr[k] && rank == pp) L[pp] = raw[k];
+                }
+#if defined(CN_ABL_NO_LP)
+                rx = L[0].x + L[8].y; ry = L[4].z + (float)cnt;   // timing-only ablation build
+#else
+                const int fail_at = lp2_r(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
+#if defined(CN_ABL_NO_LP3)
+                rx += (float)fail_at;                            // timing-only ablation build
+#else
+                if (fail_at < cnt) lp3_r(L, cnt, fail_at, my_vmax, rx, ry);
+#endif
+#endif
+            } else {
+                float rq = rangeSq;
+                int cnt = 0;
+                const int maxN = M;
+                const int T = sl.T;
+                // KdTree: persisted agents_ order (identity at simulator creation)
+                uint8_t *perm = sl.perm;
+                for (int a = 0; a < A; ++a) perm[a * T + tid] = frozen ? S.o_perm[gh * A + a] : (uint8_t)a;
+                auto AX = [&](int a) -> float {
+                    if (a == 0) return X0;
+                    float x, y, vx, vy, r;
+                    slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
+                    return x;
+                };
+                auto AY = [&](int a) -> float {
+                    if (a == 0) return Y0;
+                    float x, y, vx, vy, r;
+                    slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
+                    return y;
+                };
+                // build (buildAgentTreeRecursive), iteratively; partitions perm in place
+                int stb[CN_MAX_A], ste[CN_MAX_A], sp = 0;
+                stb[sp] = 0; ste[sp] = A; ++sp;
+                while (sp > 0) {
+                    --sp;
+                    const int b = stb[sp], e = ste[sp];
+                    if (e - b <= 10) continue;
+                    float mnx = AX(perm[b * T + tid]), mxx = mnx;
+                    float mny = AY(perm[b * T + tid]), mxy = mny;
+                    for (int q = b + 1; q < e; ++q) {
+                        const int a = perm[q * T + tid];
+                        const float x = AX(a), y = AY(a);
+                        mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
+                        mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
+                    }
+                    const bool vert = (mxx - mnx > mxy - mny);
+                    const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
+                    int left = b, right = e;
+                    while (left < right) {
+                        while (left < right) {
+                            const int a = perm[left * T + tid];
+                            if (!((vert ? AX(a) : AY(a)) < split)) break;
+                            ++left;
+                        }
+                        while (right > left) {
+                            const int a = perm[(right - 1) * T + tid];
+                            if (!((vert ? AX(a) : AY(a)) >= split)) break;
+                            --right;
+                        }
+                        if (left < right) {
+                            const uint8_t t0 = perm[left * T + tid];
+                            perm[left * T + tid] = perm[(right - 1) * T + tid];
+                            perm[(right - 1) * T + tid] = t0;
+                            ++left; --right;
+                        }
+                    }
+                    if (left == b) { ++left; }
+                    stb[sp] = b; ste[sp] = left; ++sp;
+                    stb[sp] = left; ste[sp] = e; ++sp;
+                }
+                for (int a = 0; a < A; ++a) S.o_perm[gh * A + a] = perm[a * T + tid];
+                // query (queryAgentTreeRecursive): closer child first, ties -> right; subtree pruning
+                // never drops an in-range agent, so visiting every leaf inserts the same neighbours
+                sp = 0; stb[sp] = 0; ste[sp] = A; ++sp;
+                while (sp > 0) {
+                    --sp;
+                    const int b = stb[sp], e = ste[sp];
+                    if (e - b <= 10) {
+                        for (int q = b; q < e; ++q) {
+                            const int a = perm[q * T + tid];
+                            if (a == 0) continue;
+                            const float dx = X0 - AX(a), dy = Y0 - AY(a);
+                            insert_nbr(sl, tid, cnt, maxN, a - 1, dx * dx + dy * dy, rq);
+                        }
+                        continue;
+                    }
+                    float mnx = AX(perm[b * T + tid]), mxx = mnx;
+                    float mny = AY(perm[b * T + tid]), mxy = mny;
+                    for (int q = b + 1; q < e; ++q) {
+                        const int a = perm[q * T + tid];
+                        const float x = AX(a), y = AY(a);
+                        mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
+                        mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
+                    }
+                    const bool vert = (mxx - mnx > mxy - mny);
+                    const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
+                    int left = b;
+                    for (int q = b; q < e; ++q) {
+                        const int a = perm[q * T + tid];
+                        if ((vert ? AX(a) : AY(a)) < split) ++left;
+                    }
+                    if (left == b) ++left;
+                    float bb[2][4];
+                    for (int ch = 0; ch < 2; ++ch) {
+                        const int cb = ch ? left : b, ce = ch ? e : left;
+                        float a0x = AX(perm[cb * T + tid]), a1x = a0x;
+                        float a0y = AY(perm[cb * T + tid]), a1y = a0y;
+                        for (int q = cb + 1; q < ce; ++q) {
+                            const int a = perm[q * T + tid];
+                            const float x = AX(a), y = AY(a);
+                            a1x = a1x < x ? x : a1x; a0x = x < a0x ? x : a0x;
+                            a1y = a1y < y ? y : a1y; a0y = y < a0y ? y : a0y;
+                        }
+                        bb[ch][0] = a0x; bb[ch][1] = a1x; bb[ch][2] = a0y; bb[ch][3] = a1y;
+                    }
+                    const float dl = bbox_dist(X0, Y0, bb[0][0], bb[0][1], bb[0][2], bb[0][3]);
+                    const float dr = bbox_dist(X0, Y0, bb[1][0], bb[1][1], bb[1][2], bb[1][3]);
+                    if (dl < dr) {  // visit left first: push right, then left
+                        stb[sp] = left; ste[sp] = e; ++sp; stb[sp] = b; ste[sp] = left; ++sp;
+                    } else {
+                        stb[sp] = b; ste[sp] = left; ++sp; stb[sp] = left; ste[sp] = e; ++sp;
+                    }
+                }
+                // ORCA lines in neighbour order (Agent::computeNewVelocity, agents only)
+                LineView L{sl.lines, tid, T}, PL{sl.proj, tid, T};
+                for (int pq = 0; pq < cnt; ++pq) {
+                    const int k = sl.ns[pq * T + tid];
+                    float ox, oy, ovx, ovy, orr;
+                    slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, ox, oy, ovx, ovy, orr);
+                    L.set(pq, orca_line(X0, Y0, VX0, VY0, R0, ox, oy, ovx, ovy, orr, invTH, invTS));
+                }
+                const int fail_at = lp2(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
+                if (fail_at < cnt) lp3(L, PL, cnt, fail_at, my_vmax, rx, ry);
+            }
             nvx = (double)rx; nvy = (double)ry;
         } else {
             // SOCIAL_FORCE.predict (social_force.py:11-66)
@@ -791,14 +946,19 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         // per-human terms of calc_reward (crowd_sim.py:934-969), PRE-move
         const double rdx = px - RF(sl, R_PX, el, EPB), rdy = py - RF(sl, R_PY, el, EPB);
         sl.cd[tid] = dsqrt(rdx * rdx + rdy * rdy) - rad - RF(sl, R_RAD, el, EPB);
+#if defined(CN_ABL_NO_VR)
+        uint32_t f = 0u;
+#else
         double hcx[4], hcy[4], rcx[4], rcy[4];
         vel_rect(px, py, vx0, vy0, rad, false, hcx, hcy);
         for (int k = 0; k < 4; ++k) { rcx[k] = sl.rvr[k * EPB + el]; rcy[k] = sl.rvr[(4 + k) * EPB + el]; }
         uint32_t f = quads_intersect(rcx, rcy, hcx, hcy) ? LF_VR : 0u;
+#endif
         if (!(np_norm2(px - HF(sl, H_GX, tid), py - HF(sl, H_GY, tid)) < rad)) f |= LF_NOTREACHED;
         sl.lf[tid] = f;
     }
     __syncthreads();
+    STAMP_A(3);
 
     // ---- phase 3: calc_reward ladder + robot kinematics + Monitor (env lanes) ---------------------
     if (rl) {
@@ -930,6 +1090,7 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         sl.rflag[EPB + tid] = (uint32_t)done;   // aux word: done
     }
     __syncthreads();
+    STAMP_A(4);
 
     // ---- phase 4: human kinematics, observation, goal-change detection ---------------------------
     if (hl) {
@@ -988,6 +1149,10 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
             g.work[slot] = (uint32_t)ge | (done ? 0x80000000u : 0u);
         }
     }
+#ifdef CN_STAMPS
+    __syncthreads();
+    STAMP_A(5);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -997,121 +1162,129 @@ struct RngArgs {
     cn_state_ptrs s;
     const uint32_t *work;
     const uint32_t *work_count;
+    uint32_t *next_work_count;  // zeroed here for the next step (double buffering, no memset launch)
     int reset_all;          // cn_reset: every env, done = 1
     int E;
     int64_t case_size, counter_offset;
     float *robot_node, *temporal, *spatial;
 };
 
-struct MT {
-    uint32_t *w;  // LDS [624]
-    int pos;
-    bool twisted;
-    __device__ uint32_t next()
-    {
-        if (pos >= CN_MT_N) {  // mt19937_gen, sequential (rare: once per 312 doubles)
-            int k;
-            for (k = 0; k < CN_MT_N - 397; ++k) w[k] = mt_mix(w[k], w[k + 1], w[k + 397]);
-            for (; k < CN_MT_N - 1; ++k) w[k] = mt_mix(w[k], w[k + 1], w[k + (397 - CN_MT_N)]);
-            w[CN_MT_N - 1] = mt_mix(w[CN_MT_N - 1], w[0], w[396]);
-            pos = 0;
-            twisted = true;
-        }
-        return mt_temper(w[pos++]);
-    }
-    __device__ double rnd()
-    {
-        const int32_t a = (int32_t)(next() >> 5), b = (int32_t)(next() >> 6);
-        return (a * 67108864.0 + b) / 9007199254740992.0;
-    }
-    __device__ double unif(double lo, double hi) { return lo + (hi - lo) * rnd(); }
-};
+// numpy MT19937 stream over a two-block LDS ring: block 0 = current key words, block 1 = the key after
+// the next mt19937_gen. Every lane of the (single-wave) workgroup keeps the same stream position `p`;
+// "sequential" draws are read by all lanes (LDS broadcast), and rejection loops evaluate up to 64
+// consecutive tries speculatively, one per lane, since each try consumes a fixed number of words.
 
-// wave-cooperative mt19937_gen on LDS words (64 lanes)
-__device__ inline void mt_twist_wave(uint32_t *w, int lane)
+// wave-cooperative mt19937_gen: n = gen(o) (all 64 lanes of the workgroup must call it)
+__device__ inline void mt_gen_wave(const uint32_t *o, uint32_t *n, int lane)
 {
-    uint32_t nv[4];
-    // part 1: k in [0, 227): reads old words only
-    for (int r = 0; r < 4; ++r) {
-        const int k = lane + 64 * r;
-        if (k < CN_MT_N - 397) nv[r] = mt_mix(w[k], w[k + 1], w[k + 397]);
-    }
+    for (int k = lane; k < CN_MT_N - 397; k += 64) n[k] = mt_mix(o[k], o[k + 1], o[k + 397]);
     __syncthreads();
-    for (int r = 0; r < 4; ++r) { const int k = lane + 64 * r; if (k < CN_MT_N - 397) w[k] = nv[r]; }
-    __syncthreads();
-    // part 2: k in [227, 623): w[k - 227] is new (part 1), w[k], w[k+1] old -> chunks of 227
     for (int base = CN_MT_N - 397; base < CN_MT_N - 1; base += 227) {
         const int end = min(base + 227, CN_MT_N - 1);
-        uint32_t v[4];
-        for (int r = 0; r < 4; ++r) {
-            const int k = base + lane + 64 * r;
-            if (k < end) v[r] = mt_mix(w[k], w[k + 1], w[k + (397 - CN_MT_N)]);
-        }
-        __syncthreads();
-        for (int r = 0; r < 4; ++r) { const int k = base + lane + 64 * r; if (k < end) w[k] = v[r]; }
+        for (int k = base + lane; k < end; k += 64) n[k] = mt_mix(o[k], o[k + 1], n[k + (397 - CN_MT_N)]);
         __syncthreads();
     }
-    if (lane == 0) w[CN_MT_N - 1] = mt_mix(w[CN_MT_N - 1], w[0], w[396]);
+    if (lane == 0) n[CN_MT_N - 1] = mt_mix(o[CN_MT_N - 1], n[0], n[396]);
     __syncthreads();
 }
 
-struct Env1 {  // one env's agents in LDS (kernel B)
-    double rpx, rpy, rgx, rgy, rr;
-    double *hpx, *hpy, *hgx, *hgy, *hr, *hvp, *hth;  // [N]
+__device__ __forceinline__ double mt_dbl(const uint32_t *w, int q)
+{
+    const int32_t a = (int32_t)(mt_temper(w[q]) >> 5), b = (int32_t)(mt_temper(w[q + 1]) >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+struct WRng {
+    uint32_t *w;   // LDS [2*624]
+    int p;         // stream position (wave-uniform), 0 .. 2*624
+    bool have1;    // block 1 generated
+    bool slid;     // the key advanced by at least one whole block (key words must be written back)
+    int lane;
+    // make words [p, p + need) readable (need <= 624); all lanes call it together
+    __device__ void ensure(int need)
+    {
+        if (p + need > CN_MT_N && !have1) { mt_gen_wave(w, w + CN_MT_N, lane); have1 = true; }
+        if (p + need > 2 * CN_MT_N) {
+            for (int k = lane; k < CN_MT_N; k += 64) w[k] = w[CN_MT_N + k];
+            __syncthreads();
+            mt_gen_wave(w, w + CN_MT_N, lane);
+            p -= CN_MT_N;
+            slid = true;
+        }
+    }
+    __device__ double rnd() { ensure(2); const double d = mt_dbl(w, p); p += 2; return d; }
+    __device__ double unif(double lo, double hi) { return lo + (hi - lo) * rnd(); }
 };
 
-__device__ inline double rand_world_pt(const cn_config &c, MT &m) { return (m.rnd() - 0.5) * c.square_width / 2; }
+// words one try of create_agent_attributes(scenario) consumes (crowd_sim.py:296-357)
+__host__ __device__ inline int cand_words(int scenario)
+{
+    switch (scenario) {
+    case CN_SC_CIRCLE_CROSSING: return 6;
+    case CN_SC_SQUARE_CROSSING: return 12;
+    case CN_SC_PARALLEL_TRAFFIC: case CN_SC_PERPENDICULAR_TRAFFIC: return 10;
+    default: return 6;
+    }
+}
 
-__device__ void create_agent_attributes(const cn_config &c, MT &m, int scenario, double agent_vpref, double agent_radius,
-                                        double robot_radius, double &px, double &py, double &gx, double &gy,
-                                        double &heading, double &vp)
+// create_agent_attributes from the words starting at q
+__device__ void cand_attributes(const cn_config &c, const uint32_t *w, int q, int scenario, double agent_vpref,
+                                double agent_radius, double robot_radius, double &px, double &py, double &gx,
+                                double &gy, double &heading, double &vp)
 {
     double v_pref = agent_vpref == 0 ? 1.0 : agent_vpref;
-    const double pxn = (m.rnd() - 0.5) * v_pref;
-    const double pyn = (m.rnd() - 0.5) * v_pref;
+    const double pxn = (mt_dbl(w, q) - 0.5) * v_pref;
+    const double pyn = (mt_dbl(w, q + 2) - 0.5) * v_pref;
+    q += 4;
     const double R = c.circle_radius;
+    auto rwp = [&](int qq) { return (mt_dbl(w, qq) - 0.5) * c.square_width / 2; };
     heading = 0;
     switch (scenario) {
     case CN_SC_CIRCLE_CROSSING: {
-        const double angle = m.rnd() * CN_PI * 2;
+        const double angle = mt_dbl(w, q) * CN_PI * 2;
         px = R * cos(angle) + pxn; py = R * sin(angle) + pyn;
         gx = -px; gy = -py;
     } break;
     case CN_SC_SQUARE_CROSSING:
-        px = rand_world_pt(c, m) * 0.4 + pxn;
-        py = rand_world_pt(c, m) * 0.4 + pyn;
-        gx = rand_world_pt(c, m) * 0.4 + pxn;
-        gy = rand_world_pt(c, m) * 0.4 + pyn;
+        px = rwp(q) * 0.4 + pxn;
+        py = rwp(q + 2) * 0.4 + pyn;
+        gx = rwp(q + 4) * 0.4 + pxn;
+        gy = rwp(q + 6) * 0.4 + pyn;
         break;
     case CN_SC_PARALLEL_TRAFFIC: {
-        const double sign = m.rnd() >= 0.5 ? 1 : -1;
-        px = rand_world_pt(c, m) * 0.4 + pxn;
-        py = sign * (m.rnd() * 3 + 1 + pyn);
+        const double sign = mt_dbl(w, q) >= 0.5 ? 1 : -1;
+        px = rwp(q + 2) * 0.4 + pxn;
+        py = sign * (mt_dbl(w, q + 4) * 3 + 1 + pyn);
         gx = px; gy = -py;
     } break;
     case CN_SC_PERPENDICULAR_TRAFFIC: {
-        const double sign = m.rnd() >= 0.5 ? 1 : -1;
-        px = sign * (m.rnd() * 3 + 1 + pxn);
+        const double sign = mt_dbl(w, q) >= 0.5 ? 1 : -1;
+        px = sign * (mt_dbl(w, q + 2) * 3 + 1 + pxn);
         gx = -px;
-        py = rand_world_pt(c, m) * 0.4 + pyn;
+        py = rwp(q + 4) * 0.4 + pyn;
         gy = py;
     } break;
     case CN_SC_SIDE_PREF_PASSING:
     case CN_SC_SIDE_PREF_OVERTAKING: {
         const double min_x = -(robot_radius + agent_radius), max_x = -min_x;
-        const double hx = (max_x - min_x) * m.rnd() + min_x;
+        const double hx = (max_x - min_x) * mt_dbl(w, q) + min_x;
         px = hx; gx = hx;
         if (scenario == CN_SC_SIDE_PREF_PASSING) { py = R; gy = -R; heading = -CN_PI / 2; }
         else { py = -R + 2; gy = R + 2; heading = CN_PI / 2; v_pref = 0.3; }
     } break;
     default: {
         const double min_x = -(R + robot_radius + agent_radius), max_x = -(R - robot_radius - agent_radius);
-        const double hx = (max_x - min_x) * m.rnd() + min_x;
+        const double hx = (max_x - min_x) * mt_dbl(w, q) + min_x;
         px = hx; gx = -hx; py = 0; gy = 0;
     } break;
     }
     vp = v_pref;
 }
+
+struct Env1 {  // one env's agents in LDS (kernel B)
+    double rpx, rpy, rgx, rgy, rr;
+    double *hpx, *hpy, *hgx, *hgy, *hr, *hvp, *hth;  // [N]
+};
 
 // goal candidate rejection test against the robot and all other humans (positions AND goals)
 __device__ inline bool goal_collides(const cn_config &c, const Env1 &en, int N, int self, double gx, double gy)
@@ -1127,24 +1300,56 @@ __device__ inline bool goal_collides(const cn_config &c, const Env1 &en, int N, 
     return false;
 }
 
+// Speculative rejection loop: try t = t0 + lane is evaluated by `eval(q, ok)` on the words starting
+// at q = p + W*lane; the first accepted try wins (RVO/reference order), bounded by max_tries (the
+// reference loops forever; after max_tries the last try is accepted and `overflow` is counted).
+// Returns the winning lane of the final round; the caller reads that lane's candidate from LDS.
+template <typename F>
+__device__ int wave_reject(WRng &m, int W, int max_tries, uint32_t &ovf, F eval)
+{
+    const int J = min(64, CN_MT_N / W);
+    for (int t0 = 0;; t0 += J) {
+        m.ensure(W * J);
+        const bool valid = m.lane < J && t0 + m.lane < max_tries;
+        bool ok = false;
+        if (valid) eval(m.p + W * m.lane, ok);
+        const unsigned long long mask = __ballot(valid && ok);
+        if (mask) {
+            const int first = __ffsll((long long)mask) - 1;
+            m.p += W * (first + 1);
+            return first;
+        }
+        if (t0 + J >= max_tries) {
+            const int last = max_tries - 1 - t0;
+            m.p += W * (last + 1);
+            ++ovf;
+            return last;
+        }
+        m.p += W * J;
+    }
+}
+
 __global__ void __launch_bounds__(64) cn_rng_kernel(RngArgs g, cn_config c)
 {
-    __shared__ uint32_t mtw[CN_MT_N];
+    __shared__ uint32_t mtw[2 * CN_MT_N];
     __shared__ double hbuf[7][32];
-    __shared__ double rbuf[8];
-    __shared__ uint32_t misc[4];
     const cn_state_ptrs &S = g.s;
     const int lane = threadIdx.x;
     const int N = c.human_num;
     const uint32_t nwork = g.reset_all ? (uint32_t)g.E : *g.work_count;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && g.next_work_count) *g.next_work_count = 0u;
     for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
         const uint32_t item = g.reset_all ? (w | 0x80000000u) : g.work[w];
         const int64_t e = item & 0x7fffffffu;
         const bool done = (item >> 31) != 0;
+        STAMP_B(w, 0);
         Env1 en;
         en.hpx = hbuf[0]; en.hpy = hbuf[1]; en.hgx = hbuf[2]; en.hgy = hbuf[3]; en.hr = hbuf[4]; en.hvp = hbuf[5];
         en.hth = hbuf[6];
         const int64_t hb = e * N;
+        WRng m;
+        m.w = mtw; m.have1 = false; m.slid = false; m.lane = lane;
+        uint32_t ovf = 0;
         if (!done) {
             // ---------------- goal changes (crowd_sim_dict.py:260-269) ----------------
             for (int k = lane; k < CN_MT_N; k += 64) mtw[k] = S.mt[e * CN_MT_N + k];
@@ -1153,69 +1358,84 @@ __global__ void __launch_bounds__(64) cn_rng_kernel(RngArgs g, cn_config c)
                 en.hgx[lane] = S.h_gx[hb + lane]; en.hgy[lane] = S.h_gy[hb + lane];
                 en.hr[lane] = S.h_r[hb + lane]; en.hvp[lane] = S.h_vpref[hb + lane];
             }
+            m.p = S.mt_pos[e];
+            ovf = S.overflow[e];
+            en.rpx = S.r_px[e]; en.rpy = S.r_py[e]; en.rgx = S.r_gx[e]; en.rgy = S.r_gy[e]; en.rr = S.r_radius[e];
+            const int sc = S.scenario[e];
+            const bool rgoal = c.random_goal_changing && np_mod(S.gtime[e], 5.0) == 0.0;
             __syncthreads();
-            if (lane == 0) {
-                en.rpx = S.r_px[e]; en.rpy = S.r_py[e]; en.rgx = S.r_gx[e]; en.rgy = S.r_gy[e]; en.rr = S.r_radius[e];
-                MT m{mtw, S.mt_pos[e], false};
-                uint32_t ovf = S.overflow[e];
-                const int sc = S.scenario[e];
-                if (c.random_goal_changing && np_mod(S.gtime[e], 5.0) == 0.0) {
-                    // update_human_goals_randomly (crowd_sim.py:724-766)
-                    for (int i = 0; i < N; ++i) {
-                        if (en.hvp[i] == 0) continue;
-                        if (m.rnd() <= c.goal_change_chance) {
-                            double gx = 0, gy = 0;
-                            for (int t = 0;; ++t) {
-                                const double angle = m.rnd() * CN_PI * 2;
-                                const double vp = en.hvp[i] == 0 ? 1.0 : en.hvp[i];
-                                const double gxn = (m.rnd() - 0.5) * vp, gyn = (m.rnd() - 0.5) * vp;
-                                gx = c.circle_radius * cos(angle) + gxn;
-                                gy = c.circle_radius * sin(angle) + gyn;
-                                if (!goal_collides(c, en, N, i, gx, gy)) break;
-                                if (t + 1 >= c.max_tries) { ++ovf; break; }
-                            }
-                            en.hgx[i] = gx; en.hgy[i] = gy;
+            STAMP_B(w, 1);
+            if (rgoal) {
+                // update_human_goals_randomly (crowd_sim.py:724-766): U, then tries of (angle, gx_n, gy_n)
+                for (int i = 0; i < N; ++i) {
+                    if (en.hvp[i] == 0) continue;
+                    if (m.rnd() <= c.goal_change_chance) {
+                        const double vp = en.hvp[i] == 0 ? 1.0 : en.hvp[i];
+                        wave_reject(m, 6, c.max_tries, ovf, [&](int q, bool &ok) {
+                            const double angle = mt_dbl(mtw, q) * CN_PI * 2;
+                            const double gxn = (mt_dbl(mtw, q + 2) - 0.5) * vp, gyn = (mt_dbl(mtw, q + 4) - 0.5) * vp;
+                            const double gx = c.circle_radius * cos(angle) + gxn;
+                            const double gy = c.circle_radius * sin(angle) + gyn;
+                            ok = !goal_collides(c, en, N, i, gx, gy);
+                        });
+                        // the accepted try's words end at p: recompute its candidate on every lane
+                        const int q = m.p - 6;
+                        const double angle = mt_dbl(mtw, q) * CN_PI * 2;
+                        const double gxn = (mt_dbl(mtw, q + 2) - 0.5) * vp, gyn = (mt_dbl(mtw, q + 4) - 0.5) * vp;
+                        __syncthreads();
+                        if (lane == 0) {
+                            en.hgx[i] = c.circle_radius * cos(angle) + gxn;
+                            en.hgy[i] = c.circle_radius * sin(angle) + gyn;
                         }
+                        __syncthreads();
                     }
                 }
-                if (c.end_goal_changing) {
-                    // update_human_goal (crowd_sim.py:769-811) for humans within radius of their goal
-                    for (int i = 0; i < N; ++i) {
-                        if (!(np_norm2(en.hgx[i] - en.hpx[i], en.hgy[i] - en.hpy[i]) < en.hr[i])) continue;
-                        if (m.rnd() <= c.end_goal_change_chance) {
-                            if (c.random_radii) en.hr[i] += m.unif(-0.1, 0.1);
-                            if (c.random_v_pref) en.hvp[i] += m.unif(-0.1, 0.1);
-                            double gx = 0, gy = 0;
-                            for (int t = 0;; ++t) {
-                                double px, py, hd, vp;
-                                create_agent_attributes(c, m, sc, en.hvp[i], en.hr[i], en.rr, px, py, gx, gy, hd, vp);
-                                if (!goal_collides(c, en, N, i, gx, gy)) break;
-                                if (t + 1 >= c.max_tries) { ++ovf; break; }
-                            }
-                            en.hgx[i] = gx; en.hgy[i] = gy;
-                        }
-                    }
-                }
-                S.mt_pos[e] = m.pos;
-                S.overflow[e] = ovf;
-                misc[0] = m.twisted ? 1u : 0u;
             }
-            __syncthreads();
+            if (c.end_goal_changing) {
+                // update_human_goal (crowd_sim.py:769-811) for humans within radius of their goal
+                for (int i = 0; i < N; ++i) {
+                    if (!(np_norm2(en.hgx[i] - en.hpx[i], en.hgy[i] - en.hpy[i]) < en.hr[i])) continue;
+                    if (m.rnd() <= c.end_goal_change_chance) {
+                        double r_i = en.hr[i], vp_i = en.hvp[i];
+                        if (c.random_radii) r_i += m.unif(-0.1, 0.1);
+                        if (c.random_v_pref) vp_i += m.unif(-0.1, 0.1);
+                        __syncthreads();
+                        if (lane == 0) { en.hr[i] = r_i; en.hvp[i] = vp_i; }
+                        __syncthreads();
+                        const int W = cand_words(sc);
+                        wave_reject(m, W, c.max_tries, ovf, [&](int q, bool &ok) {
+                            double px, py, gx, gy, hd, vp;
+                            cand_attributes(c, mtw, q, sc, vp_i, r_i, en.rr, px, py, gx, gy, hd, vp);
+                            ok = !goal_collides(c, en, N, i, gx, gy);
+                        });
+                        double px, py, gx, gy, hd, vp;
+                        cand_attributes(c, mtw, m.p - W, sc, vp_i, r_i, en.rr, px, py, gx, gy, hd, vp);
+                        __syncthreads();
+                        if (lane == 0) { en.hgx[i] = gx; en.hgy[i] = gy; }
+                        __syncthreads();
+                    }
+                }
+            }
+            STAMP_B(w, 2);
+            // numpy twists lazily: a stream that consumed exactly the 624 words is (old key, pos 624)
+            const bool in1 = m.p > CN_MT_N;
             if (lane < N) {
                 S.h_gx[hb + lane] = en.hgx[lane]; S.h_gy[hb + lane] = en.hgy[lane];
                 S.h_r[hb + lane] = en.hr[lane]; S.h_vpref[hb + lane] = en.hvp[lane];
             }
-            if (misc[0]) for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[k];
+            if (in1 || m.slid)
+                for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[(in1 ? CN_MT_N : 0) + k];
+            if (lane == 0) { S.mt_pos[e] = in1 ? m.p - CN_MT_N : m.p; S.overflow[e] = ovf; }
             __syncthreads();
+            STAMP_B(w, 3);
             continue;
         }
         // ---------------- CrowdSimDict.reset (crowd_sim_dict.py:105-203) ----------------
         const int64_t gidx = c.env_offset + e;
+        int sc;
+        if (c.scenario_mode == CN_SCMODE_SEQUENTIAL) sc = c.scenarios[S.reset_count[e] % c.num_scenarios];
+        else sc = c.scenarios[gidx % c.num_scenarios];
         if (lane == 0) {
-            int sc;
-            if (c.scenario_mode == CN_SCMODE_SEQUENTIAL) sc = c.scenarios[S.reset_count[e] % c.num_scenarios];
-            else sc = c.scenarios[gidx % c.num_scenarios];
-            misc[1] = (uint32_t)sc;
             uint32_t seed = (uint32_t)(g.counter_offset + S.case_counter[e] + (c.seed + gidx));
             for (int k = 0; k < CN_MT_N; ++k) {  // mt19937_seed: sequential Knuth chain
                 mtw[k] = seed;
@@ -1223,63 +1443,65 @@ __global__ void __launch_bounds__(64) cn_rng_kernel(RngArgs g, cn_config c)
             }
         }
         __syncthreads();
-        mt_twist_wave(mtw, lane);
-        if (lane == 0) {
-            MT m{mtw, 0, false};
-            const int sc = (int)misc[1];
-            uint32_t ovf = 0;
-            const double R = c.circle_radius;
-            en.rr = c.robot_radius;
-            double rth;
-            if (c.kinematics == CN_UNICYCLE) {
-                const double angle = m.unif(0, CN_PI * 2);
-                en.rpx = R * cos(angle); en.rpy = R * sin(angle);
-                for (int t = 0;; ++t) {
-                    en.rgx = m.unif(-R, R); en.rgy = m.unif(-R, R);
-                    if (np_norm2(en.rpx - en.rgx, en.rpy - en.rgy) >= 6) break;
-                    if (t + 1 >= c.max_tries) { ++ovf; break; }
-                }
-                rth = m.unif(0, 2 * CN_PI);
-            } else if (c.social_metrics || c.side_preference) {
-                en.rpx = 0; en.rpy = -R; en.rgx = 0; en.rgy = R; rth = CN_PI / 2;
-            } else {
-                for (int t = 0;; ++t) {
-                    en.rpx = m.unif(-R, R); en.rpy = m.unif(-R, R); en.rgx = m.unif(-R, R); en.rgy = m.unif(-R, R);
-                    if (np_norm2(en.rpx - en.rgx, en.rpy - en.rgy) >= 6) break;
-                    if (t + 1 >= c.max_tries) { ++ovf; break; }
-                }
-                rth = CN_PI / 2;
-            }
-            for (int i = 0; i < N; ++i) {
-                double vpref = c.human_vpref, rad = c.human_radius;
-                if (c.randomize_attributes) { vpref = m.unif(0.5, 1.5); rad = m.unif(0.3, 0.5); }
-                double px = 0, py = 0, gx = 0, gy = 0, hd = 0, vp = 0;
-                for (int t = 0;; ++t) {
-                    create_agent_attributes(c, m, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
-                    bool collide = false;
-                    for (int a = 0; a <= i; ++a) {
-                        double md, ax, ay;
-                        if (a == 0) {
-                            ax = en.rpx; ay = en.rpy;
-                            md = c.kinematics == CN_UNICYCLE ? R / 2 : rad + en.rr + c.discomfort_dist;
-                        } else {
-                            ax = en.hpx[a - 1]; ay = en.hpy[a - 1];
-                            md = rad + en.hr[a - 1] + c.discomfort_dist;
-                        }
-                        if (np_norm2(px - ax, py - ay) < md) { collide = true; break; }
+        STAMP_B(w, 1);
+        m.p = CN_MT_N;   // numpy: pos = 624 after seeding, the first draw runs mt19937_gen
+        const double R = c.circle_radius;
+        en.rr = c.robot_radius;
+        double rth;
+        if (c.kinematics == CN_UNICYCLE) {
+            const double angle = m.unif(0, CN_PI * 2);
+            en.rpx = R * cos(angle); en.rpy = R * sin(angle);
+            wave_reject(m, 4, c.max_tries, ovf, [&](int q, bool &ok) {
+                const double gx = -R + (R - -R) * mt_dbl(mtw, q), gy = -R + (R - -R) * mt_dbl(mtw, q + 2);
+                ok = np_norm2(en.rpx - gx, en.rpy - gy) >= 6;
+            });
+            en.rgx = -R + (R - -R) * mt_dbl(mtw, m.p - 4);
+            en.rgy = -R + (R - -R) * mt_dbl(mtw, m.p - 2);
+            rth = m.unif(0, 2 * CN_PI);
+        } else if (c.social_metrics || c.side_preference) {
+            en.rpx = 0; en.rpy = -R; en.rgx = 0; en.rgy = R; rth = CN_PI / 2;
+        } else {
+            wave_reject(m, 8, c.max_tries, ovf, [&](int q, bool &ok) {
+                const double px = -R + (R - -R) * mt_dbl(mtw, q), py = -R + (R - -R) * mt_dbl(mtw, q + 2);
+                const double gx = -R + (R - -R) * mt_dbl(mtw, q + 4), gy = -R + (R - -R) * mt_dbl(mtw, q + 6);
+                ok = np_norm2(px - gx, py - gy) >= 6;
+            });
+            en.rpx = -R + (R - -R) * mt_dbl(mtw, m.p - 8); en.rpy = -R + (R - -R) * mt_dbl(mtw, m.p - 6);
+            en.rgx = -R + (R - -R) * mt_dbl(mtw, m.p - 4); en.rgy = -R + (R - -R) * mt_dbl(mtw, m.p - 2);
+            rth = CN_PI / 2;
+        }
+        const int W = cand_words(sc);
+        for (int i = 0; i < N; ++i) {
+            double vpref = c.human_vpref, rad = c.human_radius;
+            if (c.randomize_attributes) { vpref = m.unif(0.5, 1.5); rad = m.unif(0.3, 0.5); }
+            wave_reject(m, W, c.max_tries, ovf, [&](int q, bool &ok) {
+                double px, py, gx, gy, hd, vp;
+                cand_attributes(c, mtw, q, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
+                bool collide = false;
+                for (int a = 0; a <= i && !collide; ++a) {
+                    double md, ax, ay;
+                    if (a == 0) {
+                        ax = en.rpx; ay = en.rpy;
+                        md = c.kinematics == CN_UNICYCLE ? R / 2 : rad + en.rr + c.discomfort_dist;
+                    } else {
+                        ax = en.hpx[a - 1]; ay = en.hpy[a - 1];
+                        md = rad + en.hr[a - 1] + c.discomfort_dist;
                     }
-                    if (!collide) break;
-                    if (t + 1 >= c.max_tries) { ++ovf; break; }
+                    if (np_norm2(px - ax, py - ay) < md) collide = true;
                 }
+                ok = !collide;
+            });
+            double px, py, gx, gy, hd, vp;
+            cand_attributes(c, mtw, m.p - W, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
+            __syncthreads();
+            if (lane == 0) {
                 en.hpx[i] = px; en.hpy[i] = py; en.hgx[i] = gx; en.hgy[i] = gy;
                 en.hth[i] = hd; en.hvp[i] = vp; en.hr[i] = rad;
             }
-            rbuf[0] = en.rpx; rbuf[1] = en.rpy; rbuf[2] = en.rgx; rbuf[3] = en.rgy; rbuf[4] = rth;
-            misc[0] = ovf;
-            misc[2] = (uint32_t)m.pos;
+            __syncthreads();
         }
-        __syncthreads();
-        const double rpx = rbuf[0], rpy = rbuf[1];
+        STAMP_B(w, 2);
+        const double rpx = en.rpx, rpy = en.rpy;
         if (lane < N) {
             const int64_t h = hb + lane;
             const double px = en.hpx[lane], py = en.hpy[lane];
@@ -1290,7 +1512,7 @@ __global__ void __launch_bounds__(64) cn_rng_kernel(RngArgs g, cn_config c)
             // generate_ob(reset=True): robot velocity is 0 (ints) -> float64 FOV path
             double fx, fy;
             if (c.kinematics == CN_HOLONOMIC) fov_dir64(atan2(0.0, 0.0), fx, fy);
-            else fov_dir64(rbuf[4], fx, fy);
+            else fov_dir64(rth, fx, fy);
             double bpx, bpy, bvx, bvy, br;
             if (in_fov(fx, fy, rpx, rpy, px, py, c.robot_fov)) { bpx = px; bpy = py; bvx = 0; bvy = 0; br = en.hr[lane]; }
             else { bpx = 15.0; bpy = 15.0; bvx = 0.0; bvy = 0.0; br = 0.3; }
@@ -1300,23 +1522,26 @@ __global__ void __launch_bounds__(64) cn_rng_kernel(RngArgs g, cn_config c)
         }
         const int A = N + (c.robot_visible ? 1 : 0);
         if (A > 10) for (int k = lane; k < N * A; k += 64) S.o_perm[e * N * A + k] = 0;
-        for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[k];
+        // the key after seeding always advanced: it is block 1 (p > 624) or block 0 after slides
+        const bool in1 = m.p > CN_MT_N;
+        for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[(in1 ? CN_MT_N : 0) + k];
         if (lane == 0) {
-            S.scenario[e] = (int32_t)misc[1];
+            S.scenario[e] = (int32_t)sc;
             S.gtime[e] = 0.0; S.r_dv[e] = 0.0;
-            S.r_px[e] = rpx; S.r_py[e] = rpy; S.r_gx[e] = rbuf[2]; S.r_gy[e] = rbuf[3]; S.r_theta[e] = rbuf[4];
+            S.r_px[e] = rpx; S.r_py[e] = rpy; S.r_gx[e] = en.rgx; S.r_gy[e] = en.rgy; S.r_theta[e] = rth;
             S.r_vx[e] = 0.0; S.r_vy[e] = 0.0; S.r_radius[e] = c.robot_radius; S.r_vpref[e] = c.robot_vpref;
             S.case_counter[e] = (S.case_counter[e] + c.nenv) % g.case_size;
-            S.potential[e] = -fabs(np_norm2(rpx - rbuf[2], rpy - rbuf[3]));
+            S.potential[e] = -fabs(np_norm2(rpx - en.rgx, rpy - en.rgy));
             S.reset_count[e] += 1;
             S.ep_return[e] = 0.0; S.ep_len[e] = 0;
-            S.flags[e] = 0; S.overflow[e] = misc[0]; S.mt_pos[e] = (int32_t)misc[2];
+            S.flags[e] = 0; S.overflow[e] = ovf; S.mt_pos[e] = in1 ? m.p - CN_MT_N : m.p;
             float *rn = g.robot_node + e * 7;
             rn[0] = (float)rpx; rn[1] = (float)rpy; rn[2] = (float)c.robot_radius;
-            rn[3] = (float)rbuf[2]; rn[4] = (float)rbuf[3]; rn[5] = (float)c.robot_vpref; rn[6] = (float)rbuf[4];
+            rn[3] = (float)en.rgx; rn[4] = (float)en.rgy; rn[5] = (float)c.robot_vpref; rn[6] = (float)rth;
             g.temporal[e * 2] = 0.0f; g.temporal[e * 2 + 1] = 0.0f;
         }
         __syncthreads();
+        STAMP_B(w, 4);
     }
 }
 
@@ -1387,6 +1612,7 @@ struct cn_engine {
     uint32_t *work_count; // [4]
     int64_t case_size, counter_offset;
     int rng_grid;
+    uint64_t nstep;
     // kernel timing (cn_profile)
     int prof_on, prof_cap, prof_n;
     hipEvent_t *ev;  // [3 * prof_cap]: before A, after A, after B
@@ -1499,8 +1725,12 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     hipMemcpyToSymbol(HIP_SYMBOL(c_circ_cos), cs, sizeof cs);
     hipMemcpyToSymbol(HIP_SYMBOL(c_circ_sin), sn, sizeof sn);
     if (g->plan.total > 160 * 1024) { cn_destroy(g); return set_err(CN_EUNSUPPORTED, "LDS plan exceeds 160 KiB"); }
-    if (g->plan.total > 64 * 1024)
-        hipFuncSetAttribute((const void *)cn_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, g->plan.total);
+    if (g->plan.total > 64 * 1024) {
+        (void)hipFuncSetAttribute((const void *)cn_step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  g->plan.total);
+        (void)hipFuncSetAttribute((const void *)cn_step_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  g->plan.total);
+    }
     g->rng_grid = g->E < 2048 ? g->E : 2048;
     HIPCHK(hipDeviceSynchronize());
     *out = g;
@@ -1563,7 +1793,8 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     if (!g || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
     RngArgs a;
-    a.s = g->s; a.work = g->work; a.work_count = g->work_count; a.reset_all = 1; a.E = g->E;
+    a.s = g->s; a.work = g->work; a.work_count = g->work_count; a.next_work_count = nullptr; a.reset_all = 1;
+    a.E = g->E;
     a.case_size = g->case_size; a.counter_offset = g->counter_offset;
     a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
     hipLaunchKernelGGL(cn_rng_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
@@ -1576,19 +1807,24 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
 {
     if (!g || !actions || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    HIPCHK(hipMemsetAsync(g->work_count, 0, 16, st));
+    uint32_t *cnt = g->work_count + (g->nstep & 1);        // zeroed by the previous step's kernel B
+    uint32_t *cnt_next = g->work_count + ((g->nstep + 1) & 1);
+    ++g->nstep;
     const bool prof = g->prof_on && g->prof_n < g->prof_cap;
     if (prof) HIPCHK(hipEventRecord(g->ev[3 * g->prof_n], st));
     StepArgs a;
     a.s = g->s; a.actions = actions; a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
     a.reward = reward; a.done = done; a.event = event; a.info = info; a.ep_return = ep_return; a.ep_len = ep_len;
-    a.work = g->work; a.work_count = g->work_count; a.E = g->E;
+    a.work = g->work; a.work_count = cnt; a.E = g->E;
     const int blocks = (g->E + g->plan.EPB - 1) / g->plan.EPB;
-    hipLaunchKernelGGL(cn_step_kernel, dim3(blocks), dim3(CN_BLK), g->plan.total, st, a, g->c);
+    if (g->plan.kd)
+        hipLaunchKernelGGL(cn_step_kernel<true>, dim3(blocks), dim3(g->plan.T), g->plan.total, st, a, g->c);
+    else
+        hipLaunchKernelGGL(cn_step_kernel<false>, dim3(blocks), dim3(g->plan.T), g->plan.total, st, a, g->c);
     HIPCHK(hipGetLastError());
     if (prof) HIPCHK(hipEventRecord(g->ev[3 * g->prof_n + 1], st));
     RngArgs b;
-    b.s = g->s; b.work = g->work; b.work_count = g->work_count; b.reset_all = 0; b.E = g->E;
+    b.s = g->s; b.work = g->work; b.work_count = cnt; b.next_work_count = cnt_next; b.reset_all = 0; b.E = g->E;
     b.case_size = g->case_size; b.counter_offset = g->counter_offset;
     b.robot_node = robot_node; b.temporal = temporal; b.spatial = spatial;
     hipLaunchKernelGGL(cn_rng_kernel, dim3(g->rng_grid), dim3(64), 0, st, b, g->c);
@@ -1634,6 +1870,16 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
     }
     return CN_OK;
 }
+
+#ifdef CN_STAMPS
+int cn_debug_stamps(unsigned long long *a, unsigned long long *b)
+{
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(a, HIP_SYMBOL(cn_stamp_a), sizeof(unsigned long long) * 4096 * CN_NSTAMP));
+    HIPCHK(hipMemcpyFromSymbol(b, HIP_SYMBOL(cn_stamp_b), sizeof(unsigned long long) * 8192 * CN_NSTAMP));
+    return CN_OK;
+}
+#endif
 
 int cn_edge_features(void *stream, int64_t E, int N, const float *robot_node, const float *temporal_edges,
                      const float *spatial_edges, const float *Wt, const float *bt, const float *Ws, const float *bs,

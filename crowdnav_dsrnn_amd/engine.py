@@ -15,7 +15,7 @@ class CrowdNavEngine:
     """E environments of the reference's CrowdSimDict on one GPU.
 
     reset()                  -> obs dict (robot_node (E,1,7), temporal_edges (E,1,2), spatial_edges (E,N,2))
-    step(actions (E,2) f32)  -> obs, reward (E,), done (E,) bool, event (E,) int8, info (E,K), ep_return (E,) f64,
+    step(actions (E,2) f32)  -> obs, reward (E,), done (E,) uint8, event (E,) int8, info (E,K), ep_return (E,) f64,
                                 ep_len (E,) i32       (auto-reset of finished envs, like the reference VecEnv)
     Returned tensors are the engine's own buffers (overwritten by the next call); clone to keep them.
     """
@@ -75,7 +75,7 @@ class CrowdNavEngine:
                 self.temporal_edges.data_ptr(), self.spatial_edges.data_ptr(), self.reward.data_ptr(),
                 self.done.data_ptr(), self.event.data_ptr(), self.info.data_ptr(), self.ep_return.data_ptr(),
                 self.ep_len.data_ptr()))
-        return self.obs(), self.reward, self.done.bool(), self.event, self.info, self.ep_return, self.ep_len
+        return self.obs(), self.reward, self.done, self.event, self.info, self.ep_return, self.ep_len
 
     # -------------------------------------------------------------------------------------------
     def get_state(self):

@@ -224,6 +224,9 @@ static int lp2(const rline *L, int n, float radius, float ox, float oy, int dirO
     return n;
 }
 
+static long long g_cnt_lp2 = 0, g_cnt_lp3 = 0, g_cnt_lines = 0;
+EXPORT void cnref_debug_counters(long long *out) { out[0] = g_cnt_lp2; out[1] = g_cnt_lp3; out[2] = g_cnt_lines; }
+
 /* linearProgram3 (numObstLines = 0) */
 static void lp3(const rline *L, int n, int begin, float radius, float *rx, float *ry)
 {
@@ -412,7 +415,9 @@ static void rvo2_agent0(int A, const float *X, const float *Y, const float *VX, 
     }
     float rx, ry;
     const int fail_at = lp2(L, cnt, vmax, prefx, prefy, 0, &rx, &ry);
-    if (fail_at < cnt) lp3(L, cnt, fail_at, vmax, &rx, &ry);
+    __atomic_add_fetch(&g_cnt_lp2, 1, __ATOMIC_RELAXED);
+    __atomic_add_fetch(&g_cnt_lines, cnt, __ATOMIC_RELAXED);
+    if (fail_at < cnt) { lp3(L, cnt, fail_at, vmax, &rx, &ry); __atomic_add_fetch(&g_cnt_lp3, 1, __ATOMIC_RELAXED); }
     *outx = rx; *outy = ry;
 }
 

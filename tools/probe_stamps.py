@@ -1,0 +1,76 @@
+"""Diagnostic: phase breakdown of the step and RNG kernels from the -DCN_STAMPS build.
+
+    CN_LIB_PATH=crowdnav_dsrnn_amd/lib/libcrowdnav_hip_stamps.so python tools/probe_stamps.py [variant]
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from crowdnav_dsrnn_amd import _lib  # noqa: E402
+from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config  # noqa: E402
+from crowdnav_dsrnn_amd.engine import CrowdNavEngine  # noqa: E402
+
+
+def run(variant, E=4096, N=10, steps=60):
+    c = clone_config(Config())
+    c.sim.human_num = N
+    c.sim.train_val_sim = ["circle_crossing"]
+    c.action_space.kinematics = "unicycle"
+    if variant == "nogoal":
+        c.humans.random_goal_changing = False
+        c.humans.end_goal_changing = False
+    if variant == "sf":
+        c.humans.policy = "social_force"
+    eng = CrowdNavEngine(make_cn_config(c, num_envs=E), "cuda:0")
+    eng.reset()
+    L = _lib.lib()
+    L.cn_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    a = np.zeros(4096 * 8, np.uint64)
+    b = np.zeros(8192 * 8, np.uint64)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(0)
+    acts = torch.rand((steps, E, 2), generator=g, device="cuda:0") * 0.2 - 0.1
+    _lib.check(L.cn_profile(eng._h, 1, steps))
+    for s in range(steps):
+        eng.step(acts[s])
+    torch.cuda.synchronize()
+    ta, tb, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    L.cn_profile_read(eng._h, ctypes.byref(ta), ctypes.byref(tb), ctypes.byref(n))
+    L.cn_debug_stamps(a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p))
+    blocks = (E + (256 // N) - 1) // (256 // N)
+    A = a.reshape(-1, 8)[:blocks].astype(np.int64)
+    d = np.diff(A[:, :6], axis=1)
+    print("[%s] kernel A avg %.1f us, kernel B avg %.1f us over %d steps" % (variant, ta.value * 1e3 / n.value,
+                                                                          tb.value * 1e3 / n.value, n.value))
+    names = ["load", "visibility", "policy+reward terms", "reward ladder", "kinematics+obs+worklist"]
+    tot = (A[:, 5] - A[:, 0])
+    print("  kernel A cycles per workgroup (last step): total median %d max %d" % (np.median(tot), tot.max()))
+    for k, nm in enumerate(names):
+        print("    %-26s median %8d  max %8d  (%.0f%%)" % (nm, np.median(d[:, k]), d[:, k].max(),
+                                                            100 * np.median(d[:, k]) / np.median(tot)))
+    cnt = int(eng.done.sum().item())
+    B = b.reshape(-1, 8).astype(np.int64)
+    used = B[:, 0] > 0
+    Bu = B[used]
+    # items: reset items have stamp 4 set; goal items stop at 3
+    res = Bu[Bu[:, 4] > 0]
+    goal = Bu[Bu[:, 4] == 0]
+    if len(res):
+        r = np.diff(res[:, :5], axis=1)
+        print("  kernel B reset items (cumulative over run, %d): seed %d  twist %d  spawn %d  write %d  (median cycles)" % (
+            len(res), *np.median(r, axis=0)))
+        print("     reset total max %d" % (res[:, 4] - res[:, 0]).max())
+    if len(goal):
+        gg = np.diff(goal[:, :4], axis=1)
+        print("  kernel B goal items (%d): load %d  lane0 %d  write %d (median cycles); lane0 max %d" % (
+            len(goal), *np.median(gg, axis=0), gg[:, 1].max()))
+    eng.close()
+
+
+if __name__ == "__main__":
+    for v in (sys.argv[1:] or ["c2", "nogoal", "sf"]):
+        run(v)
