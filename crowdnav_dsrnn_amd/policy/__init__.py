@@ -1,0 +1,3 @@
+"""DSRNN policy (reference: pytorchBaselines/a2c_ppo_acktr/{model,srnn_model,distributions}.py)."""
+from .model import Policy  # noqa: F401
+from .srnn_model import SRNN  # noqa: F401

@@ -1,0 +1,136 @@
+"""DSRNN policy vs the reference (tests/golden/dsrnn.npz: reference Policy.act / evaluate_actions on
+procedural weights, pytorchBaselines/a2c_ppo_acktr/model.py:63-104).
+
+CPU tests check the module tree / state_dict against the reference's key list and run the whole
+policy graph with the fused input-layer kernel replaced by its plain fp32 torch restatement; the GPU
+tests run the real HIP kernel (cn_edge_features) and compare to the same fixture.
+Tolerance: 2e-5 abs + 1e-4 rel on value / action / log-prob / hidden states (fp32 GEMM/GRU
+summation-order differences between MIOpen/rocBLAS and the reference's CPU kernels)."""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import edge_features_fp32, load, make_policy
+
+ATOL, RTOL = 2e-5, 1e-4
+
+
+@pytest.fixture(scope="module")
+def dsrnn():
+    return load("dsrnn.npz")
+
+
+def _obs(d, p, dev):
+    return {k: torch.from_numpy(d[p + k]).to(dev) for k in ("robot_node", "temporal_edges", "spatial_edges")}
+
+
+def _run_act(d, N, dev):
+    pol = make_policy(N, device=dev)
+    p = "N%d_act_" % N
+    obs = _obs(d, p + "obs_", dev)
+    hxs = {k: torch.from_numpy(d[p + "hxs_" + k].copy()).to(dev) for k in ("human_node_rnn", "human_human_edge_rnn")}
+    with torch.no_grad():
+        v, a, lp, nh = pol.act(obs, hxs, torch.from_numpy(d[p + "masks"]).to(dev), deterministic=True)
+    return v, a, lp, nh
+
+
+def _check_act(d, N, out):
+    v, a, lp, nh = out
+    p = "N%d_act_" % N
+    np.testing.assert_allclose(v.cpu().numpy(), d[p + "value"], atol=ATOL, rtol=RTOL)
+    np.testing.assert_allclose(a.cpu().numpy(), d[p + "action"], atol=ATOL, rtol=RTOL)
+    np.testing.assert_allclose(lp.cpu().numpy(), d[p + "logp"], atol=ATOL, rtol=RTOL)
+    for k in ("human_node_rnn", "human_human_edge_rnn"):
+        assert tuple(nh[k].shape) == d[p + "new_" + k].shape
+        np.testing.assert_allclose(nh[k].cpu().numpy(), d[p + "new_" + k], atol=ATOL, rtol=RTOL)
+
+
+def _run_eval(d, N, dev):
+    pol = make_policy(N, device=dev)
+    p = "N%d_ev_" % N
+    obs = _obs(d, p + "obs_", dev)
+    hxs = {k: torch.from_numpy(d[p + "hxs_" + k].copy()).to(dev) for k in ("human_node_rnn", "human_human_edge_rnn")}
+    with torch.no_grad():
+        return pol.evaluate_actions(obs, hxs, torch.from_numpy(d[p + "masks"]).to(dev),
+                                    torch.from_numpy(d[p + "actions"]).to(dev))
+
+
+def _check_eval(d, N, out):
+    v, lp, ent, _ = out
+    p = "N%d_ev_" % N
+    np.testing.assert_allclose(v.cpu().numpy(), d[p + "value"], atol=ATOL, rtol=RTOL)
+    np.testing.assert_allclose(lp.cpu().numpy(), d[p + "logp"], atol=ATOL, rtol=RTOL)
+    np.testing.assert_allclose(float(ent), float(d[p + "entropy"]), atol=ATOL, rtol=RTOL)
+
+
+@pytest.mark.parametrize("N", [5, 10])
+def test_state_dict_matches_reference_keys(dsrnn, N):
+    pol = make_policy(N)
+    sd = pol.state_dict()
+    assert sorted(sd.keys()) == list(dsrnn["N%d_keys" % N])
+    assert [str(tuple(v.shape)) for _, v in sorted(sd.items())] == list(dsrnn["N%d_shapes" % N])
+
+
+def test_fused_kernel_is_mandatory():
+    """On CPU tensors the product path fails loudly (no silent torch fallback)."""
+    from crowdnav_dsrnn_amd import ops
+
+    pol = make_policy(5)
+    d = load("dsrnn.npz")
+    with pytest.raises(ops.EdgeFeaturesUnavailable):
+        _run_act(d, 5, "cpu")
+    del pol
+
+
+@pytest.mark.parametrize("N", [5, 10])
+def test_policy_graph_cpu_with_fp32_input_layers(dsrnn, N, monkeypatch):
+    """Everything but the fused kernel, on CPU: act + evaluate_actions (mid-sequence episode starts)."""
+    from crowdnav_dsrnn_amd import ops
+
+    monkeypatch.setattr(ops, "edge_features", edge_features_fp32)
+    _check_act(dsrnn, N, _run_act(dsrnn, N, "cpu"))
+    _check_eval(dsrnn, N, _run_eval(dsrnn, N, "cpu"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [5, 10])
+def test_policy_act_gpu(dsrnn, N):
+    _check_act(dsrnn, N, _run_act(dsrnn, N, "cuda:0"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [5, 10])
+def test_policy_evaluate_actions_gpu(dsrnn, N):
+    _check_eval(dsrnn, N, _run_eval(dsrnn, N, "cuda:0"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("E,N", [(1, 1), (7, 5), (4096, 10), (300, 20)])
+def test_edge_features_kernel_vs_fp32(E, N):
+    from crowdnav_dsrnn_amd import ops
+
+    g = torch.Generator().manual_seed(E * 100 + N)
+    dev = "cuda:0"
+    args = [torch.randn(s, generator=g) * 2 for s in
+            [(E, 1, 7), (E, 1, 2), (E, N, 2), (64, 2), (64,), (64, 2), (64,), (3, 7), (3,), (64, 3), (64,)]]
+    ref = edge_features_fp32(*args)
+    out = ops.edge_features(*[a.to(dev) for a in args])
+    for r, o in zip(ref, out):
+        np.testing.assert_allclose(o.cpu().numpy(), r.numpy(), atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_edge_features_backward_vs_fp32():
+    from crowdnav_dsrnn_amd import ops
+
+    g = torch.Generator().manual_seed(3)
+    E, N = 33, 6
+    shapes = [(E, 1, 7), (E, 1, 2), (E, N, 2), (64, 2), (64,), (64, 2), (64,), (3, 7), (3,), (64, 3), (64,)]
+    base = [torch.randn(s, generator=g) for s in shapes]
+    w = [torch.randn(s, generator=g) for s in [(E, 64), (E, N, 64), (E, 64)]]
+    a_cpu = [b.clone().requires_grad_(True) for b in base]
+    sum((o * wi).sum() for o, wi in zip(edge_features_fp32(*a_cpu), w)).backward()
+    a_gpu = [b.to("cuda:0").requires_grad_(True) for b in base]
+    sum((o * wi.to("cuda:0")).sum() for o, wi in zip(ops.edge_features(*a_gpu), w)).backward()
+    for x, y in zip(a_cpu, a_gpu):
+        np.testing.assert_allclose(y.grad.cpu().numpy(), x.grad.numpy(), atol=1e-4, rtol=1e-4)
