@@ -65,7 +65,7 @@ def cpu_baseline(N, budget_s=12.0):
         eng.step(rng.uniform(-0.1, 0.1, (E, 2)).astype(np.float32))
         steps += 1
         el = time.perf_counter() - t0
-        if el > budget_s or steps >= 2000:
+        if el > budget_s or steps >= 50000:
             break
     return {"value": E * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": "oracle/cpu_ref.c (C restatement of CrowdSimDict.step incl. RVO2 ORCA), 1 thread, "
