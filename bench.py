@@ -169,7 +169,6 @@ def main():
                 "envs_per_gpu": E, "humans": N, "global_envs": E * world,
                 "parallelism": "env-sharded x%d (no collective)" % world,
                 "step_kernel_ms": round(kernel_s * 1e3, 5),
-                "rng_kernel_ms": round(b_ms.value / max(n.value, 1), 5),
             },
             "roofline": {
                 "bound": "hbm",

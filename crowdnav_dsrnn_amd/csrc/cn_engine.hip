@@ -1,17 +1,15 @@
 // cn_engine.hip — MI355X (gfx950) batched CrowdSimDict engine: kernels + C ABI (include/crowdnav.h).
 //
-// Hot path per cn_step (one HIP stream, no host synchronisation):
-//   1. cn_step_kernel   (kernel A)           — one lane per (env, human), 256-lane workgroups holding
-//                                              floor(256/N) whole envs: SRNN.clip_action, the human
-//                                              policies (ORCA LP / social force) on the PRE-move state,
-//                                              calc_reward, kinematics, observation, Monitor; envs that
-//                                              need random numbers (reset, goal changes) are appended
-//                                              to a device worklist.
-//   2. cn_rng_kernel    (kernel B)           — one wave per listed env: numpy-legacy MT19937 in LDS,
-//                                              update_human_goals_randomly / update_human_goal, and the
-//                                              VecEnv auto-reset (CrowdSimDict.reset: reseed + spawn +
-//                                              first observation). Worklist counters are double
-//                                              buffered: kernel B zeroes the next step's counter.
+// Hot path: ONE kernel launch per cn_step (no host synchronisation, no second kernel):
+//   cn_step_kernel, workgroups [0, step_blocks): one lane per (env, human), 256-lane workgroups holding
+//       floor(256/N) whole envs. Phases 0-4: SRNN.clip_action, the human policies (ORCA LP / social
+//       force) on the PRE-move state, calc_reward, kinematics, observation, Monitor. Phase 5: the
+//       workgroup's own RNG work, one wave per env needing it — goal changes (numpy-legacy MT19937 in
+//       LDS) and the VecEnv auto-reset, which copies a spawn drawn ahead of time.
+//   cn_step_kernel, workgroups [step_blocks, +pend_blocks): spawn waves. CrowdSimDict.reset is a pure
+//       function of the seed schedule, so each env's NEXT episode is drawn (reseed + spawn with
+//       rejection) by these spare workgroups right after its reset, concurrently with the step.
+//   cn_reset_kernel: cn_reset (every env), one wave per env.
 // Reference: crowd_sim/envs/crowd_sim_dict.py:105-271, crowd_sim/envs/crowd_sim.py:296-1161,
 // crowd_sim/envs/utils/agent.py:172-218, crowd_nav/policy/{orca,social_force,srnn}.py; RVO2 v2.0
 // (third-party) restated in float32. Numerics: see cn_math.h.
@@ -35,7 +33,7 @@ using namespace cn;
 __device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 #define STAMP_A(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + (k)] = clock64(); } while (0)
-#define STAMP_B(w, k) do { if (threadIdx.x == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
+#define STAMP_B(w, k) do { if ((threadIdx.x & 63) == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
 #else
 #define STAMP_A(k) do { } while (0)
 #define STAMP_B(w, k) do { } while (0)
@@ -545,6 +543,638 @@ __device__ __forceinline__ float4 orca_line(float X0, float Y0, float VX0, float
 }
 
 // ------------------------------------------------------------------------------------------------
+// RNG work (goal changes, spawn): numpy legacy MT19937 per env, one wave per env
+// ------------------------------------------------------------------------------------------------
+// Pending next-episode spawns. CrowdSimDict.reset (crowd_sim_dict.py:105-203) is a pure function of the
+// seed schedule (offset + case_counter + thisSeed) and the scenario, both fixed as soon as the previous
+// reset has run, so the spawn of env e's NEXT episode is drawn ahead of time by spare waves of kernel A
+// (off the critical path) and kernel B's auto-reset only copies it. (case_counter, reset_count) is
+// the validity key: a stale entry (e.g. after cn_set_state) is never used, the reset is then drawn inline.
+struct PendPtrs {
+    uint32_t *mt;   // [E][624] key words after the spawn draws
+    int32_t *pos;   // [E] stream position
+    uint32_t *ovf;  // [E] bounded-rejection overflows of the spawn
+    int32_t *sc;    // [E] scenario
+    int64_t *cc;    // [E] key: case_counter the spawn was drawn for
+    int32_t *rc;    // [E] key: reset_count (sequential scenario mode)
+    uint32_t *ok;   // [E] entry written
+    double *r;      // [5][E] robot px, py, gx, gy, theta
+    double *h;      // [7][E*N] human px, py, gx, gy, radius, v_pref, theta
+};
+
+// where a reset writes: state + the first observation of the new episode
+struct ResetOut {
+    cn_state_ptrs s;
+    float *robot_node, *temporal, *spatial;
+    int64_t case_size;
+};
+
+struct RngArgs {   // cn_reset_kernel
+    ResetOut o;
+    PendPtrs pend;
+    int E;
+    int64_t counter_offset;
+};
+
+// LDS ordering among the lanes of ONE wave (kernel B workgroups are a single wave; the spawn waves of
+// kernel A run independently of the other waves of their workgroup): no s_barrier needed, only the
+// compiler/LDS ordering a release/acquire pair at wavefront scope gives.
+__device__ __forceinline__ void wsync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// numpy MT19937 stream over a two-block LDS ring: block 0 = current key words, block 1 = the key after
+// the next mt19937_gen. Every lane of the (single-wave) workgroup keeps the same stream position `p`;
+// "sequential" draws are read by all lanes (LDS broadcast), and rejection loops evaluate up to 64
+// consecutive tries speculatively, one per lane, since each try consumes a fixed number of words.
+
+// wave-cooperative mt19937_gen: n = gen(o) (all 64 lanes of the workgroup must call it)
+__device__ inline void mt_gen_wave(const uint32_t *o, uint32_t *n, int lane)
+{
+    for (int k = lane; k < CN_MT_N - 397; k += 64) n[k] = mt_mix(o[k], o[k + 1], o[k + 397]);
+    wsync();
+    for (int base = CN_MT_N - 397; base < CN_MT_N - 1; base += 227) {
+        const int end = min(base + 227, CN_MT_N - 1);
+        for (int k = base + lane; k < end; k += 64) n[k] = mt_mix(o[k], o[k + 1], n[k + (397 - CN_MT_N)]);
+        wsync();
+    }
+    if (lane == 0) n[CN_MT_N - 1] = mt_mix(o[CN_MT_N - 1], n[0], n[396]);
+    wsync();
+}
+
+__device__ __forceinline__ double mt_dbl(const uint32_t *w, int q)
+{
+    const int32_t a = (int32_t)(mt_temper(w[q]) >> 5), b = (int32_t)(mt_temper(w[q + 1]) >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+struct WRng {
+    double *sl;    // LDS [6][64] per-try candidate slots (wave_reject2)
+    uint32_t *w;   // LDS [2*624]
+    int p;         // stream position (wave-uniform), 0 .. 2*624
+    bool have1;    // block 1 generated
+    bool slid;     // the key advanced by at least one whole block (key words must be written back)
+    int lane;
+    // make words [p, p + need) readable (need <= 624); all lanes call it together
+    __device__ void ensure(int need)
+    {
+        if (p + need > CN_MT_N && !have1) { mt_gen_wave(w, w + CN_MT_N, lane); have1 = true; }
+        if (p + need > 2 * CN_MT_N) {
+            for (int k = lane; k < CN_MT_N; k += 64) w[k] = w[CN_MT_N + k];
+            wsync();
+            mt_gen_wave(w, w + CN_MT_N, lane);
+            p -= CN_MT_N;
+            slid = true;
+        }
+    }
+    __device__ double rnd() { ensure(2); const double d = mt_dbl(w, p); p += 2; return d; }
+    __device__ double unif(double lo, double hi) { return lo + (hi - lo) * rnd(); }
+};
+
+// words one try of create_agent_attributes(scenario) consumes (crowd_sim.py:296-357)
+__host__ __device__ inline int cand_words(int scenario)
+{
+    switch (scenario) {
+    case CN_SC_CIRCLE_CROSSING: return 6;
+    case CN_SC_SQUARE_CROSSING: return 12;
+    case CN_SC_PARALLEL_TRAFFIC: case CN_SC_PERPENDICULAR_TRAFFIC: return 10;
+    default: return 6;
+    }
+}
+
+// create_agent_attributes from the words starting at q
+__device__ void cand_attributes(const cn_config &c, const uint32_t *w, int q, int scenario, double agent_vpref,
+                                double agent_radius, double robot_radius, double &px, double &py, double &gx,
+                                double &gy, double &heading, double &vp)
+{
+    double v_pref = agent_vpref == 0 ? 1.0 : agent_vpref;
+    const double pxn = (mt_dbl(w, q) - 0.5) * v_pref;
+    const double pyn = (mt_dbl(w, q + 2) - 0.5) * v_pref;
+    q += 4;
+    const double R = c.circle_radius;
+    auto rwp = [&](int qq) { return (mt_dbl(w, qq) - 0.5) * c.square_width / 2; };
+    heading = 0;
+    switch (scenario) {
+    case CN_SC_CIRCLE_CROSSING: {
+        const double angle = mt_dbl(w, q) * CN_PI * 2;
+        px = R * cos(angle) + pxn; py = R * sin(angle) + pyn;
+        gx = -px; gy = -py;
+    } break;
+    case CN_SC_SQUARE_CROSSING:
+        px = rwp(q) * 0.4 + pxn;
+        py = rwp(q + 2) * 0.4 + pyn;
+        gx = rwp(q + 4) * 0.4 + pxn;
+        gy = rwp(q + 6) * 0.4 + pyn;
+        break;
+    case CN_SC_PARALLEL_TRAFFIC: {
+        const double sign = mt_dbl(w, q) >= 0.5 ? 1 : -1;
+        px = rwp(q + 2) * 0.4 + pxn;
+        py = sign * (mt_dbl(w, q + 4) * 3 + 1 + pyn);
+        gx = px; gy = -py;
+    } break;
+    case CN_SC_PERPENDICULAR_TRAFFIC: {
+        const double sign = mt_dbl(w, q) >= 0.5 ? 1 : -1;
+        px = sign * (mt_dbl(w, q + 2) * 3 + 1 + pxn);
+        gx = -px;
+        py = rwp(q + 4) * 0.4 + pyn;
+        gy = py;
+    } break;
+    case CN_SC_SIDE_PREF_PASSING:
+    case CN_SC_SIDE_PREF_OVERTAKING: {
+        const double min_x = -(robot_radius + agent_radius), max_x = -min_x;
+        const double hx = (max_x - min_x) * mt_dbl(w, q) + min_x;
+        px = hx; gx = hx;
+        if (scenario == CN_SC_SIDE_PREF_PASSING) { py = R; gy = -R; heading = -CN_PI / 2; }
+        else { py = -R + 2; gy = R + 2; heading = CN_PI / 2; v_pref = 0.3; }
+    } break;
+    default: {
+        const double min_x = -(R + robot_radius + agent_radius), max_x = -(R - robot_radius - agent_radius);
+        const double hx = (max_x - min_x) * mt_dbl(w, q) + min_x;
+        px = hx; gx = -hx; py = 0; gy = 0;
+    } break;
+    }
+    vp = v_pref;
+}
+
+struct Env1 {  // one env's agents in LDS (kernel B)
+    double rpx, rpy, rgx, rgy, rr;
+    double *hpx, *hpy, *hgx, *hgy, *hr, *hvp, *hth;  // [N]
+};
+
+// One agent test of the goal rejection loops (crowd_sim.py:744-760, 792-806): does goal candidate
+// (gx, gy) of human `self` (radius r_self) come within r_self + r_agent + discomfort_dist of agent a's
+// position or goal? a = 0 is the robot, a >= 1 the other humans in index order (self skipped).
+__device__ __forceinline__ bool goal_hit(const cn_config &c, const Env1 &en, int self, double r_self, double gx,
+                                         double gy, int a)
+{
+    double ax, ay, agx, agy, ar;
+    if (a == 0) { ax = en.rpx; ay = en.rpy; agx = en.rgx; agy = en.rgy; ar = en.rr; }
+    else {
+        const int j = a - 1 < self ? a - 1 : a;
+        ax = en.hpx[j]; ay = en.hpy[j]; agx = en.hgx[j]; agy = en.hgy[j]; ar = en.hr[j];
+    }
+    const double md = r_self + ar + c.discomfort_dist;
+    return norm_lt(gx - ax, gy - ay, md) || norm_lt(gx - agx, gy - agy, md);
+}
+
+// Rejection loop of the reference (`while True: draw; if not collide: break`) with the tries AND the
+// agent tests spread over the wave: lane = (try t, agent a), t = lane / NA, a = lane % NA, so
+// J = 64 / NA consecutive tries are evaluated per pass (each try consumes W words, so try t's words
+// start at p + W*t). `cand(q, t)` runs on the a == 0 lane of each try and leaves the candidate in slot
+// t of m.sl; `hit(t, a)` is one agent test (true = collision). The first try without a hit wins, as
+// in the reference. Bounded by max_tries (the reference loops forever; after max_tries the last try
+// is accepted and `ovf` counts it). Returns the winning slot; m.p is after its words.
+template <typename FC, typename FT>
+__device__ int wave_reject2(WRng &m, int W, int NA, int max_tries, uint32_t &ovf, FC cand, FT hit)
+{
+    const int lane = m.lane;
+    const int J = min(64 / NA, CN_MT_N / W);
+    const int t = lane / NA, a = lane - t * NA;
+    const uint64_t gmask = NA >= 64 ? ~0ull : ((1ull << NA) - 1ull);
+    for (int t0 = 0;; t0 += J) {
+        m.ensure(W * J);
+        const int nt = min(J, max_tries - t0);
+        const bool valid = t < nt;
+        if (valid && a == 0) cand(m.p + W * t, t);
+        wsync();
+        const bool bad = valid && hit(t, a);
+        const uint64_t badm = __ballot(bad);
+        int first = -1;
+        for (int k = 0; k < nt; ++k)
+            if (((badm >> (k * NA)) & gmask) == 0) { first = k; break; }
+        if (first >= 0) { m.p += W * (first + 1); return first; }
+        if (t0 + J >= max_tries) { m.p += W * nt; ++ovf; return nt - 1; }
+        m.p += W * J;
+        wsync();   // slots are rewritten by the next pass
+    }
+}
+
+#define CN_PEND_LDS (2 * CN_MT_N * 4 + 7 * 32 * 8 + 6 * 64 * 8)   // per RNG wave: MT ring, agent table, try slots
+
+// The random part of CrowdSimDict.reset (crowd_sim_dict.py:110-156; generate_robot_humans,
+// crowd_sim.py:555-663; generate_circle_crossing_human :359-393): reseed the env's stream with
+// counter_offset + case_counter + thisSeed, draw the robot and then each human with rejection.
+// One wave; the result is left in `en` (LDS), rth, ovf, sc and the stream `m`.
+__device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int64_t case_counter, int32_t reset_count,
+                          int64_t counter_offset, WRng &m, Env1 &en, double &rth, uint32_t &ovf, int &sc)
+{
+    const int lane = m.lane;
+    const int N = c.human_num;
+    uint32_t *mtw = m.w;
+    if (c.scenario_mode == CN_SCMODE_SEQUENTIAL) sc = c.scenarios[reset_count % c.num_scenarios];
+    else sc = c.scenarios[gidx % c.num_scenarios];
+    if (lane == 0) {
+        uint32_t seed = (uint32_t)(counter_offset + case_counter + (c.seed + gidx));
+        for (int k = 0; k < CN_MT_N; ++k) {  // mt19937_seed: sequential Knuth chain
+            mtw[k] = seed;
+            seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(k + 1);
+        }
+    }
+    wsync();
+    m.p = CN_MT_N;   // numpy: pos = 624 after seeding, the first draw runs mt19937_gen
+    m.have1 = false; m.slid = false;
+    ovf = 0;
+    const double R = c.circle_radius;
+    en.rr = c.robot_radius;
+    if (c.kinematics == CN_UNICYCLE) {
+        const double angle = m.unif(0, CN_PI * 2);
+        en.rpx = R * cos(angle); en.rpy = R * sin(angle);
+        // goal: uniform in the square until >= 6 m away (crowd_sim.py:620-634)
+        const int tw = wave_reject2(m, 4, 1, c.max_tries, ovf, [&](int q, int t) {
+            m.sl[t] = -R + (R - -R) * mt_dbl(mtw, q); m.sl[64 + t] = -R + (R - -R) * mt_dbl(mtw, q + 2);
+        }, [&](int t, int) { return norm_lt(en.rpx - m.sl[t], en.rpy - m.sl[64 + t], 6.0); });
+        en.rgx = m.sl[tw]; en.rgy = m.sl[64 + tw];
+        wsync();
+        rth = m.unif(0, 2 * CN_PI);
+    } else if (c.social_metrics || c.side_preference) {
+        en.rpx = 0; en.rpy = -R; en.rgx = 0; en.rgy = R; rth = CN_PI / 2;
+    } else {
+        // holonomic robot: start and goal uniform in the square until >= 6 m apart (crowd_sim.py:652-660)
+        const int tw = wave_reject2(m, 8, 1, c.max_tries, ovf, [&](int q, int t) {
+            m.sl[t] = -R + (R - -R) * mt_dbl(mtw, q); m.sl[64 + t] = -R + (R - -R) * mt_dbl(mtw, q + 2);
+            m.sl[128 + t] = -R + (R - -R) * mt_dbl(mtw, q + 4); m.sl[192 + t] = -R + (R - -R) * mt_dbl(mtw, q + 6);
+        }, [&](int t, int) { return norm_lt(m.sl[t] - m.sl[128 + t], m.sl[64 + t] - m.sl[192 + t], 6.0); });
+        en.rpx = m.sl[tw]; en.rpy = m.sl[64 + tw]; en.rgx = m.sl[128 + tw]; en.rgy = m.sl[192 + tw];
+        wsync();
+        rth = CN_PI / 2;
+    }
+    const int W = cand_words(sc);
+    for (int i = 0; i < N; ++i) {
+        double vpref = c.human_vpref, rad = c.human_radius;
+        if (c.randomize_attributes) { vpref = m.unif(0.5, 1.5); rad = m.unif(0.3, 0.5); }
+        // candidate vs the robot and the humans placed so far (crowd_sim.py:369-390): i + 1 agent tests
+        const int tw = wave_reject2(m, W, i + 1, c.max_tries, ovf, [&](int q, int t) {
+            double px, py, gx, gy, hd, vp;
+            cand_attributes(c, mtw, q, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
+            m.sl[t] = px; m.sl[64 + t] = py; m.sl[128 + t] = gx; m.sl[192 + t] = gy; m.sl[256 + t] = hd;
+            m.sl[320 + t] = vp;
+        }, [&](int t, int a) {
+            double md, ax, ay;
+            if (a == 0) {
+                ax = en.rpx; ay = en.rpy;
+                md = c.kinematics == CN_UNICYCLE ? R / 2 : rad + en.rr + c.discomfort_dist;
+            } else {
+                ax = en.hpx[a - 1]; ay = en.hpy[a - 1];
+                md = rad + en.hr[a - 1] + c.discomfort_dist;
+            }
+            return norm_lt(m.sl[t] - ax, m.sl[64 + t] - ay, md);
+        });
+        if (lane == 0) {
+            en.hpx[i] = m.sl[tw]; en.hpy[i] = m.sl[64 + tw]; en.hgx[i] = m.sl[128 + tw]; en.hgy[i] = m.sl[192 + tw];
+            en.hth[i] = m.sl[256 + tw]; en.hvp[i] = m.sl[320 + tw]; en.hr[i] = rad;
+        }
+        wsync();
+    }
+}
+
+// Store a drawn spawn as env e's pending next episode.
+__device__ __forceinline__ void write_pending(const PendPtrs &P, const cn_config &c, int64_t E, int64_t e, const Env1 &en, double rth,
+                              int sc, uint32_t ovf, const uint32_t *mt_src, int pos, int64_t cc, int32_t rc, int lane)
+{
+    const int N = c.human_num;
+    for (int k = lane; k < CN_MT_N; k += 64) P.mt[e * CN_MT_N + k] = mt_src[k];
+    if (lane < N) {
+        const int64_t h = e * N + lane, EN = E * N;
+        P.h[h] = en.hpx[lane]; P.h[EN + h] = en.hpy[lane]; P.h[2 * EN + h] = en.hgx[lane];
+        P.h[3 * EN + h] = en.hgy[lane]; P.h[4 * EN + h] = en.hr[lane]; P.h[5 * EN + h] = en.hvp[lane];
+        P.h[6 * EN + h] = en.hth[lane];
+    }
+    if (lane == 0) {
+        P.r[e] = en.rpx; P.r[E + e] = en.rpy; P.r[2 * E + e] = en.rgx; P.r[3 * E + e] = en.rgy; P.r[4 * E + e] = rth;
+        P.pos[e] = pos; P.ovf[e] = ovf; P.sc[e] = sc; P.cc[e] = cc; P.rc[e] = rc;
+        P.ok[e] = 1u;
+    }
+}
+
+// The deterministic rest of CrowdSimDict.reset (crowd_sim_dict.py:136-203): state of the new episode,
+// case_counter advance, first observation. `mt_src` = key words after the spawn (LDS or pending buffer).
+__device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &c, int64_t e, const Env1 &en, double rth, int sc,
+                            uint32_t ovf, const uint32_t *mt_src, int pos, int lane)
+{
+    const cn_state_ptrs &S = g.s;
+    const int N = c.human_num;
+    const int64_t hb = e * N;
+    const double rpx = en.rpx, rpy = en.rpy;
+    if (lane < N) {
+        const int64_t h = hb + lane;
+        const double px = en.hpx[lane], py = en.hpy[lane];
+        S.h_px[h] = px; S.h_py[h] = py; S.h_gx[h] = en.hgx[lane]; S.h_gy[h] = en.hgy[lane];
+        S.h_vx[h] = 0.0; S.h_vy[h] = 0.0; S.h_r[h] = en.hr[lane]; S.h_vpref[h] = en.hvp[lane];
+        S.h_theta[h] = en.hth[lane];
+        S.o_r[h] = 0.0f; S.o_vmax[h] = 0.0f; S.o_dmask[h] = 0u;
+        // generate_ob(reset=True): robot velocity is 0 (ints) -> float64 FOV path
+        double fx, fy;
+        if (c.kinematics == CN_HOLONOMIC) fov_dir64(atan2(0.0, 0.0), fx, fy);
+        else fov_dir64(rth, fx, fy);
+        double bpx, bpy, bvx, bvy, br;
+        if (in_fov(fx, fy, rpx, rpy, px, py, c.robot_fov)) { bpx = px; bpy = py; bvx = 0; bvy = 0; br = en.hr[lane]; }
+        else { bpx = 15.0; bpy = 15.0; bvx = 0.0; bvy = 0.0; br = 0.3; }
+        S.b_px[h] = bpx; S.b_py[h] = bpy; S.b_vx[h] = bvx; S.b_vy[h] = bvy; S.b_r[h] = br;
+        g.spatial[h * 2] = (float)(bpx - rpx);
+        g.spatial[h * 2 + 1] = (float)(bpy - rpy);
+    }
+    const int A = N + (c.robot_visible ? 1 : 0);
+    if (A > 10) for (int k = lane; k < N * A; k += 64) S.o_perm[e * N * A + k] = 0;
+    for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mt_src[k];
+    if (lane == 0) {
+        S.scenario[e] = (int32_t)sc;
+        S.gtime[e] = 0.0; S.r_dv[e] = 0.0;
+        S.r_px[e] = rpx; S.r_py[e] = rpy; S.r_gx[e] = en.rgx; S.r_gy[e] = en.rgy; S.r_theta[e] = rth;
+        S.r_vx[e] = 0.0; S.r_vy[e] = 0.0; S.r_radius[e] = c.robot_radius; S.r_vpref[e] = c.robot_vpref;
+        S.case_counter[e] = (S.case_counter[e] + c.nenv) % g.case_size;
+        S.potential[e] = -fabs(np_norm2(rpx - en.rgx, rpy - en.rgy));
+        S.reset_count[e] += 1;
+        S.ep_return[e] = 0.0; S.ep_len[e] = 0;
+        S.flags[e] = 0; S.overflow[e] = ovf; S.mt_pos[e] = pos;
+        float *rn = g.robot_node + e * 7;
+        rn[0] = (float)rpx; rn[1] = (float)rpy; rn[2] = (float)c.robot_radius;
+        rn[3] = (float)en.rgx; rn[4] = (float)en.rgy; rn[5] = (float)c.robot_vpref; rn[6] = (float)rth;
+        g.temporal[e * 2] = 0.0f; g.temporal[e * 2 + 1] = 0.0f;
+    }
+}
+
+
+// One of the two goal-change loops at the end of CrowdSimDict.step, evaluated speculatively:
+//   KIND 0  update_human_goals_randomly (crowd_sim.py:724-766): humans with v_pref != 0 draw U; if
+//           U <= goal_change_chance a new goal on the circle is rejection-sampled (angle, gx_noise, gy_noise);
+//   KIND 1  update_human_goal (crowd_sim.py:769-811): humans within their radius of the goal draw U; if
+//           U <= end_goal_change_chance radius / v_pref are jittered and create_agent_attributes'
+//           candidate is rejection-sampled.
+// Both walk the humans in index order. If every changing human accepts its FIRST try, the word position
+// of every draw is fixed: the walk becomes a table of U values (lane = (eligible human k, changes
+// before it c), one draw each) plus a scalar scan, and all first tries are tested at once, lane =
+// (changing human, agent), each against the goals the earlier humans then have. Up to the first human
+// whose first try is rejected this IS the sequential result; that human runs the ordinary rejection
+// loop (wave_reject2) and the walk resumes after it. `sp`: wave LDS scratch, 3*32 doubles.
+template <int KIND>
+__device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, uint32_t &ovf, int sc, double *sp)
+{
+    int dbg = 0;   // diagnostics: 1000 * rounds + eligible humans + 100 * changes
+    const int N = c.human_num, lane = m.lane;
+    uint32_t *mtw = m.w;
+    double *ngx = sp, *ngy = sp + 32, *nr = sp + 64;
+    const double chance = KIND == 0 ? c.goal_change_chance : c.end_goal_change_chance;
+    const int W = KIND == 0 ? 6 : cand_words(sc);
+    const int JW = KIND == 0 ? 0 : 2 * ((c.random_radii ? 1 : 0) + (c.random_v_pref ? 1 : 0));
+    const int SW = JW + W;     // words of one accepted-first-try change after its U
+    bool elig_l = false;       // eligibility reads only the human's own goal / radius: fixed up front
+    if (lane < N) {
+        if (KIND == 0) elig_l = en.hvp[lane] != 0;
+        else elig_l = norm_lt(en.hgx[lane] - en.hpx[lane], en.hgy[lane] - en.hpy[lane], en.hr[lane]);
+    }
+    const uint64_t elig = __ballot(elig_l);
+    dbg += __popcll(elig);
+    int i0 = 0;
+    while (i0 < N) {
+        const uint64_t rem = elig & (~0ull << i0);
+        if (!rem) break;
+        dbg += 1000;
+        const int n = __popcll(rem);
+        m.ensure(n * (2 + SW));
+        const int p0 = m.p;
+        // ---- walk: U of the k-th eligible human sits at p0 + 2k + SW*c, c = changes before it
+        uint64_t chg = 0;
+        int posl = -1, cnum = 0;
+        if (n * (n + 1) / 2 <= 64) {
+            int k = 0, cc = lane;
+            while (cc > k) { cc -= k + 1; ++k; }
+            const bool dec = lane < n * (n + 1) / 2 && mt_dbl(mtw, p0 + 2 * k + SW * cc) <= chance;
+            const uint64_t B = __ballot(dec);
+            uint64_t mm = rem;
+            for (int kk = 0; kk < n; ++kk) {
+                const int h = __ffsll((long long)mm) - 1;
+                mm &= mm - 1;
+                if ((B >> (kk * (kk + 1) / 2 + cnum)) & 1ull) {
+                    chg |= 1ull << h;
+                    if (lane == h) posl = p0 + 2 * (kk + 1) + SW * cnum;
+                    ++cnum;
+                }
+            }
+        } else {
+            int p = p0;
+            for (int i = i0; i < N; ++i) {
+                if (!((rem >> i) & 1ull)) continue;
+                const double U = mt_dbl(mtw, p);
+                p += 2;
+                if (U <= chance) {
+                    chg |= 1ull << i;
+                    if (lane == i) posl = p;
+                    p += SW;
+                    ++cnum;
+                }
+            }
+        }
+        const int pend = p0 + 2 * n + SW * cnum;
+        if (!chg) { m.p = pend; break; }
+        dbg += 100 * __popcll(chg);
+        // ---- first tries: candidate per changing human (its lane), then lane = (candidate, agent)
+        const bool mine = lane < N && ((chg >> lane) & 1ull);
+        double r_i = 0, vp_i = 0;
+        if (mine) {
+            int q = posl;
+            double gx, gy;
+            r_i = en.hr[lane]; vp_i = en.hvp[lane];
+            if (KIND == 0) {
+                const double vp = en.hvp[lane] == 0 ? 1.0 : en.hvp[lane];
+                const double angle = mt_dbl(mtw, q) * CN_PI * 2;
+                const double gxn = (mt_dbl(mtw, q + 2) - 0.5) * vp, gyn = (mt_dbl(mtw, q + 4) - 0.5) * vp;
+                gx = c.circle_radius * cos(angle) + gxn;
+                gy = c.circle_radius * sin(angle) + gyn;
+            } else {
+                if (c.random_radii) { r_i += -0.1 + (0.1 - -0.1) * mt_dbl(mtw, q); q += 2; }
+                if (c.random_v_pref) { vp_i += -0.1 + (0.1 - -0.1) * mt_dbl(mtw, q); q += 2; }
+                double px, py, hd, vpo;
+                cand_attributes(c, mtw, q, sc, vp_i, r_i, en.rr, px, py, gx, gy, hd, vpo);
+            }
+            ngx[lane] = gx; ngy[lane] = gy; nr[lane] = r_i;
+        }
+        wsync();
+        const int NA = N;                      // robot + the other N-1 humans
+        const int CPP = 64 / NA;               // candidates per pass
+        const int ncand = __popcll(chg);
+        int f = 64;
+        for (int c0 = 0; c0 < ncand && f == 64; c0 += CPP) {
+            const int ci = lane / NA, a = lane - ci * NA;
+            int h = -1;
+            if (ci < CPP && c0 + ci < ncand) {
+                uint64_t mm = chg;
+                for (int k = 0; k < c0 + ci; ++k) mm &= mm - 1;
+                h = __ffsll((long long)mm) - 1;
+            }
+            bool bad = false;
+            if (h >= 0) {
+                // agents: robot, then humans in order; earlier changing humans already carry new goals
+                double ax, ay, agx, agy, ar;
+                if (a == 0) { ax = en.rpx; ay = en.rpy; agx = en.rgx; agy = en.rgy; ar = en.rr; }
+                else {
+                    const int j = a - 1 < h ? a - 1 : a;
+                    ax = en.hpx[j]; ay = en.hpy[j];
+                    if (j < h && ((chg >> j) & 1ull)) { agx = ngx[j]; agy = ngy[j]; ar = nr[j]; }
+                    else { agx = en.hgx[j]; agy = en.hgy[j]; ar = en.hr[j]; }
+                }
+                const double md = nr[h] + ar + c.discomfort_dist;
+                bad = norm_lt(ngx[h] - ax, ngy[h] - ay, md) || norm_lt(ngx[h] - agx, ngy[h] - agy, md);
+            }
+            const uint64_t badm = __ballot(bad);
+            const uint64_t gmask = NA >= 64 ? ~0ull : ((1ull << NA) - 1ull);
+            for (int k = 0; k < CPP && c0 + k < ncand; ++k) {
+                if ((badm >> (k * NA)) & gmask) {
+                    uint64_t mm = chg;
+                    for (int q = 0; q < c0 + k; ++q) mm &= mm - 1;
+                    f = __ffsll((long long)mm) - 1;
+                    break;
+                }
+            }
+        }
+        if (mine && lane < f) {
+            en.hgx[lane] = ngx[lane]; en.hgy[lane] = ngy[lane];
+            if (KIND == 1) { en.hr[lane] = r_i; en.hvp[lane] = vp_i; }
+        }
+        wsync();
+        if (f == 64) { m.p = pend; break; }
+        // ---- human f rejected its first try: the ordinary rejection loop from that try on
+        const int qf = __shfl(posl, f);
+        const double rf = __shfl(r_i, f), vpf = __shfl(vp_i, f);
+        if (KIND == 1 && lane == 0) { en.hr[f] = rf; en.hvp[f] = vpf; }
+        wsync();
+        m.p = qf + JW;   // its candidate words follow the U draw and the radius / v_pref jitter draws
+        const double r_self = KIND == 1 ? rf : en.hr[f];
+        const double vpk0 = en.hvp[f] == 0 ? 1.0 : en.hvp[f];
+        const int tw = wave_reject2(m, W, NA, c.max_tries, ovf, [&](int q, int t) {
+            double gx, gy;
+            if (KIND == 0) {
+                const double angle = mt_dbl(mtw, q) * CN_PI * 2;
+                const double gxn = (mt_dbl(mtw, q + 2) - 0.5) * vpk0, gyn = (mt_dbl(mtw, q + 4) - 0.5) * vpk0;
+                gx = c.circle_radius * cos(angle) + gxn;
+                gy = c.circle_radius * sin(angle) + gyn;
+            } else {
+                double px, py, hd, vp;
+                cand_attributes(c, mtw, q, sc, vpf, rf, en.rr, px, py, gx, gy, hd, vp);
+            }
+            m.sl[t] = gx; m.sl[64 + t] = gy;
+        }, [&](int t, int a) { return goal_hit(c, en, f, r_self, m.sl[t], m.sl[64 + t], a); });
+        if (lane == 0) { en.hgx[f] = m.sl[tw]; en.hgy[f] = m.sl[64 + tw]; }
+        wsync();
+        i0 = f + 1;
+    }
+    return dbg;
+}
+
+// Goal changes at the end of CrowdSimDict.step (crowd_sim_dict.py:260-269) for one env, one wave:
+// update_human_goals_randomly when `rgoal`, then update_human_goal when `egoal` (goal_pass).
+// `en` holds the post-move agents (LDS); the env's MT19937 stream is loaded from / written back to
+// the state; `sp` = wave LDS scratch.
+__device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_ptrs &S, int64_t e, Env1 &en, WRng &m,
+                                             bool rgoal, bool egoal, double *sp)
+{
+    const int N = c.human_num;
+    const int lane = m.lane;
+    uint32_t *mtw = m.w;
+    const int64_t hb = e * N;
+    for (int k = lane; k < CN_MT_N; k += 64) mtw[k] = S.mt[e * CN_MT_N + k];
+    m.p = S.mt_pos[e];
+    m.have1 = false; m.slid = false;
+    uint32_t ovf = S.overflow[e];
+    const int sc = S.scenario[e];
+    wsync();
+    STAMP_B(e, 1);
+    int dbg0 = 0, dbg1 = 0;
+    if (rgoal) dbg0 = goal_pass<0>(c, en, m, ovf, sc, sp);
+    STAMP_B(e, 2);
+    if (egoal) dbg1 = goal_pass<1>(c, en, m, ovf, sc, sp);
+    STAMP_B(e, 3);
+#ifdef CN_STAMPS
+    if (lane == 0 && e < 8192) { cn_stamp_b[e * CN_NSTAMP + 6] = dbg0; cn_stamp_b[e * CN_NSTAMP + 7] = dbg1; }
+#endif
+    (void)dbg0; (void)dbg1;
+    // numpy twists lazily: a stream that consumed exactly the 624 words is (old key, pos 624)
+    const bool in1 = m.p > CN_MT_N;
+    if (lane < N) {
+        S.h_gx[hb + lane] = en.hgx[lane]; S.h_gy[hb + lane] = en.hgy[lane];
+        S.h_r[hb + lane] = en.hr[lane]; S.h_vpref[hb + lane] = en.hvp[lane];
+    }
+    if (in1 || m.slid)
+        for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[(in1 ? CN_MT_N : 0) + k];
+    if (lane == 0) { S.mt_pos[e] = in1 ? m.p - CN_MT_N : m.p; S.overflow[e] = ovf; }
+    wsync();
+    STAMP_B(e, 4);
+}
+
+// Auto-reset of env e (VecEnv worker, shmem_vec_env.py:164-168 -> CrowdSimDict.reset): copy the pending
+// spawn when `may_consume` and it is valid for the current key, else draw it here. One wave.
+__device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P, const cn_config &c, int64_t E, int64_t e,
+                          int64_t counter_offset, bool may_consume, WRng &m, Env1 &en)
+{
+    const cn_state_ptrs &S = o.s;
+    const int N = c.human_num;
+    const int lane = m.lane;
+    const int64_t cc = S.case_counter[e];
+    const int32_t rc = S.reset_count[e];
+    if (may_consume && P.ok[e] && P.cc[e] == cc && P.rc[e] == rc) {
+        if (lane < N) {
+            const int64_t h = e * N + lane, EN = E * N;
+            en.hpx[lane] = P.h[h]; en.hpy[lane] = P.h[EN + h]; en.hgx[lane] = P.h[2 * EN + h];
+            en.hgy[lane] = P.h[3 * EN + h]; en.hr[lane] = P.h[4 * EN + h]; en.hvp[lane] = P.h[5 * EN + h];
+            en.hth[lane] = P.h[6 * EN + h];
+        }
+        en.rpx = P.r[e]; en.rpy = P.r[E + e]; en.rgx = P.r[2 * E + e]; en.rgy = P.r[3 * E + e];
+        const double rth = P.r[4 * E + e];
+        wsync();
+        write_reset(o, c, e, en, rth, P.sc[e], P.ovf[e], P.mt + e * CN_MT_N, P.pos[e], lane);
+    } else {
+        double rth;
+        uint32_t ovf;
+        int sc;
+        spawn_env(c, c.env_offset + e, cc, rc, counter_offset, m, en, rth, ovf, sc);
+        const bool in1 = m.p > CN_MT_N;
+        write_reset(o, c, e, en, rth, sc, ovf, m.w + (in1 ? CN_MT_N : 0), in1 ? m.p - CN_MT_N : m.p, lane);
+    }
+    wsync();
+}
+
+// Spawn waves of kernel A: draw the next episode of every env reset by the previous kernel A
+// (or of every env after cn_reset / cn_set_state). One wave per env, independent of the other waves.
+struct PendLaunch {
+    PendPtrs P;
+    const uint32_t *list;   // envs reset by the previous kernel B
+    const uint32_t *count;
+    int all;                // 1: every env (list ignored)
+    int step_blocks, pend_blocks;
+    int64_t counter_offset;
+};
+
+__device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_ptrs &S, const cn_config &c, int E, char *smem)
+{
+    const int nw = blockDim.x / 64, w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    char *base = smem + w * CN_PEND_LDS;
+    uint32_t *mtw = (uint32_t *)base;
+    double *hb = (double *)(base + 2 * CN_MT_N * 4);
+    const uint32_t n = pl.all ? (uint32_t)E : *pl.count;
+    for (uint32_t it = (uint32_t)((blockIdx.x - pl.step_blocks) * nw + w); it < n; it += (uint32_t)(pl.pend_blocks * nw)) {
+        const int64_t e = pl.all ? (int64_t)it : (int64_t)pl.list[it];
+        Env1 en;
+        en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
+        en.hth = hb + 192;
+        WRng m;
+        m.w = mtw; m.lane = lane;
+        m.sl = (double *)(base + 2 * CN_MT_N * 4 + 7 * 32 * 8);
+        const int64_t cc = S.case_counter[e];
+        const int32_t rc = S.reset_count[e];
+        double rth;
+        uint32_t ovf;
+        int sc;
+        spawn_env(c, c.env_offset + e, cc, rc, pl.counter_offset, m, en, rth, ovf, sc);
+        const bool in1 = m.p > CN_MT_N;
+        write_pending(pl.P, c, E, e, en, rth, sc, ovf, mtw + (in1 ? CN_MT_N : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
+                      lane);
+        wsync();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // kernel A
 // ------------------------------------------------------------------------------------------------
 struct StepArgs {
@@ -557,8 +1187,11 @@ struct StepArgs {
     float *info;
     double *ep_return;
     int32_t *ep_len;
-    uint32_t *work;
-    uint32_t *work_count;   // this step's counter (work_counts[step & 1])
+    uint32_t *plist_w;      // envs reset by this launch (their next spawn is drawn by the next launch)
+    uint32_t *pcount_w;
+    uint32_t *pcount_zero;  // the counter the NEXT launch appends to (triple-buffered), zeroed here
+    PendLaunch pend;        // spawn waves: workgroups [step_blocks, step_blocks + pend_blocks)
+    int64_t case_size;
     int E;
 };
 
@@ -615,6 +1248,11 @@ template <bool KD>
 __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
+    if ((int)blockIdx.x >= g.pend.step_blocks) {  // spare workgroups: draw upcoming episodes' spawns
+        pend_waves(g.pend, g.s, c, g.E, smem);
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *g.pcount_zero = 0u;
     const int N = c.human_num;
     const StepPlan P = cn_step_plan(N, c.robot_visible);
     const int EPB = P.EPB, M = P.M, A = P.A;
@@ -1113,6 +1751,7 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         if (np_norm2(HF(sl, H_GX, tid) - npx, HF(sl, H_GY, tid) - npy) < HF(sl, H_R, tid)) f |= LF_ENDGOAL;
         if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
         sl.lf[tid] = f;
+        HF(sl, H_PX, tid) = npx; HF(sl, H_PY, tid) = npy;   // post-move positions for the goal changes
     }
     __syncthreads();
     if (rl) {
@@ -1144,404 +1783,72 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         const bool done = sl.rflag[EPB + tid] != 0;
         const bool rgoal = c.random_goal_changing && np_mod(gt, 5.0) == 0.0;
         const bool egoal = c.end_goal_changing && endg;
-        if (done || rgoal || egoal) {
-            const uint32_t slot = atomicAdd(g.work_count, 1u);
-            g.work[slot] = (uint32_t)ge | (done ? 0x80000000u : 0u);
+        sl.rflag[EPB + tid] = (done ? 1u : 0u) | (rgoal ? 2u : 0u) | (egoal ? 4u : 0u) |
+                              (S.ep_len[ge] == 1 ? 8u : 0u);
+    }
+    __syncthreads();
+    STAMP_A(5);
+
+    // ---- phase 5: this workgroup's RNG work, one wave per env needing it --------------------------
+    // Done envs auto-reset (VecEnv worker, shmem_vec_env.py:164-168) from the pending spawn drawn by an
+    // earlier launch; an env reset by the previous launch (ep_len == 1) may be redrawn by this launch's
+    // spawn waves right now, so it (and every env after cn_reset/cn_set_state) draws inline instead.
+    {
+        const int nw = sl.T / 64, w = tid / 64, lane = tid & 63;
+        char *wb = smem + P.o_lines + w * CN_PEND_LDS;   // over the ORCA scratch, dead after phase 2
+        WRng m;
+        m.w = (uint32_t *)wb; m.lane = lane;
+        m.sl = (double *)(wb + 2 * CN_MT_N * 4 + 7 * 32 * 8);
+        double *hb = (double *)(wb + 2 * CN_MT_N * 4);
+        ResetOut o;
+        o.s = S; o.robot_node = g.robot_node; o.temporal = g.temporal; o.spatial = g.spatial; o.case_size = g.case_size;
+        int j = 0;
+        for (int q = 0; q < nenv_here; ++q) {
+            const uint32_t need = sl.rflag[EPB + q] & 7u;
+            if (!need) continue;
+            if ((j++ % nw) != w) continue;
+            const int64_t e = e0 + q;
+            STAMP_B(e, 0);
+            Env1 en;
+            if (need & 1u) {
+                en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
+                en.hth = hb + 192;
+                const bool may = !g.pend.all && !(sl.rflag[EPB + q] & 8u);
+                reset_env(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, m, en);
+                if (lane == 0) g.plist_w[atomicAdd(g.pcount_w, 1u)] = (uint32_t)e;
+                STAMP_B(e, 5);
+            } else {
+                const int b = q * N;
+                en.hpx = &HF(sl, H_PX, b); en.hpy = &HF(sl, H_PY, b); en.hgx = &HF(sl, H_GX, b);
+                en.hgy = &HF(sl, H_GY, b); en.hr = &HF(sl, H_R, b); en.hvp = &HF(sl, H_VP, b); en.hth = &HF(sl, H_TH, b);
+                en.rpx = RF(sl, R_NX, q, EPB); en.rpy = RF(sl, R_NY, q, EPB);
+                en.rgx = RF(sl, R_GX, q, EPB); en.rgy = RF(sl, R_GY, q, EPB); en.rr = RF(sl, R_RAD, q, EPB);
+                // update_human_goal checks every human AFTER the random changes (a new random goal may
+                // land within reach of its own human), so it runs whenever end goal changing is on
+                goal_changes(c, S, e, en, m, (need & 2u) != 0, c.end_goal_changing != 0, hb);
+            }
         }
     }
 #ifdef CN_STAMPS
     __syncthreads();
-    STAMP_A(5);
+    STAMP_A(6);
 #endif
 }
 
-// ------------------------------------------------------------------------------------------------
-// kernel B: RNG work (goal changes, auto-reset) — one 64-lane workgroup per listed env
-// ------------------------------------------------------------------------------------------------
-struct RngArgs {
-    cn_state_ptrs s;
-    const uint32_t *work;
-    const uint32_t *work_count;
-    uint32_t *next_work_count;  // zeroed here for the next step (double buffering, no memset launch)
-    int reset_all;          // cn_reset: every env, done = 1
-    int E;
-    int64_t case_size, counter_offset;
-    float *robot_node, *temporal, *spatial;
-};
-
-// numpy MT19937 stream over a two-block LDS ring: block 0 = current key words, block 1 = the key after
-// the next mt19937_gen. Every lane of the (single-wave) workgroup keeps the same stream position `p`;
-// "sequential" draws are read by all lanes (LDS broadcast), and rejection loops evaluate up to 64
-// consecutive tries speculatively, one per lane, since each try consumes a fixed number of words.
-
-// wave-cooperative mt19937_gen: n = gen(o) (all 64 lanes of the workgroup must call it)
-__device__ inline void mt_gen_wave(const uint32_t *o, uint32_t *n, int lane)
-{
-    for (int k = lane; k < CN_MT_N - 397; k += 64) n[k] = mt_mix(o[k], o[k + 1], o[k + 397]);
-    __syncthreads();
-    for (int base = CN_MT_N - 397; base < CN_MT_N - 1; base += 227) {
-        const int end = min(base + 227, CN_MT_N - 1);
-        for (int k = base + lane; k < end; k += 64) n[k] = mt_mix(o[k], o[k + 1], n[k + (397 - CN_MT_N)]);
-        __syncthreads();
-    }
-    if (lane == 0) n[CN_MT_N - 1] = mt_mix(o[CN_MT_N - 1], n[0], n[396]);
-    __syncthreads();
-}
-
-__device__ __forceinline__ double mt_dbl(const uint32_t *w, int q)
-{
-    const int32_t a = (int32_t)(mt_temper(w[q]) >> 5), b = (int32_t)(mt_temper(w[q + 1]) >> 6);
-    return (a * 67108864.0 + b) / 9007199254740992.0;
-}
-
-struct WRng {
-    uint32_t *w;   // LDS [2*624]
-    int p;         // stream position (wave-uniform), 0 .. 2*624
-    bool have1;    // block 1 generated
-    bool slid;     // the key advanced by at least one whole block (key words must be written back)
-    int lane;
-    // make words [p, p + need) readable (need <= 624); all lanes call it together
-    __device__ void ensure(int need)
-    {
-        if (p + need > CN_MT_N && !have1) { mt_gen_wave(w, w + CN_MT_N, lane); have1 = true; }
-        if (p + need > 2 * CN_MT_N) {
-            for (int k = lane; k < CN_MT_N; k += 64) w[k] = w[CN_MT_N + k];
-            __syncthreads();
-            mt_gen_wave(w, w + CN_MT_N, lane);
-            p -= CN_MT_N;
-            slid = true;
-        }
-    }
-    __device__ double rnd() { ensure(2); const double d = mt_dbl(w, p); p += 2; return d; }
-    __device__ double unif(double lo, double hi) { return lo + (hi - lo) * rnd(); }
-};
-
-// words one try of create_agent_attributes(scenario) consumes (crowd_sim.py:296-357)
-__host__ __device__ inline int cand_words(int scenario)
-{
-    switch (scenario) {
-    case CN_SC_CIRCLE_CROSSING: return 6;
-    case CN_SC_SQUARE_CROSSING: return 12;
-    case CN_SC_PARALLEL_TRAFFIC: case CN_SC_PERPENDICULAR_TRAFFIC: return 10;
-    default: return 6;
-    }
-}
-
-// create_agent_attributes from the words starting at q
-__device__ void cand_attributes(const cn_config &c, const uint32_t *w, int q, int scenario, double agent_vpref,
-                                double agent_radius, double robot_radius, double &px, double &py, double &gx,
-                                double &gy, double &heading, double &vp)
-{
-    double v_pref = agent_vpref == 0 ? 1.0 : agent_vpref;
-    const double pxn = (mt_dbl(w, q) - 0.5) * v_pref;
-    const double pyn = (mt_dbl(w, q + 2) - 0.5) * v_pref;
-    q += 4;
-    const double R = c.circle_radius;
-    auto rwp = [&](int qq) { return (mt_dbl(w, qq) - 0.5) * c.square_width / 2; };
-    heading = 0;
-    switch (scenario) {
-    case CN_SC_CIRCLE_CROSSING: {
-        const double angle = mt_dbl(w, q) * CN_PI * 2;
-        px = R * cos(angle) + pxn; py = R * sin(angle) + pyn;
-        gx = -px; gy = -py;
-    } break;
-    case CN_SC_SQUARE_CROSSING:
-        px = rwp(q) * 0.4 + pxn;
-        py = rwp(q + 2) * 0.4 + pyn;
-        gx = rwp(q + 4) * 0.4 + pxn;
-        gy = rwp(q + 6) * 0.4 + pyn;
-        break;
-    case CN_SC_PARALLEL_TRAFFIC: {
-        const double sign = mt_dbl(w, q) >= 0.5 ? 1 : -1;
-        px = rwp(q + 2) * 0.4 + pxn;
-        py = sign * (mt_dbl(w, q + 4) * 3 + 1 + pyn);
-        gx = px; gy = -py;
-    } break;
-    case CN_SC_PERPENDICULAR_TRAFFIC: {
-        const double sign = mt_dbl(w, q) >= 0.5 ? 1 : -1;
-        px = sign * (mt_dbl(w, q + 2) * 3 + 1 + pxn);
-        gx = -px;
-        py = rwp(q + 4) * 0.4 + pyn;
-        gy = py;
-    } break;
-    case CN_SC_SIDE_PREF_PASSING:
-    case CN_SC_SIDE_PREF_OVERTAKING: {
-        const double min_x = -(robot_radius + agent_radius), max_x = -min_x;
-        const double hx = (max_x - min_x) * mt_dbl(w, q) + min_x;
-        px = hx; gx = hx;
-        if (scenario == CN_SC_SIDE_PREF_PASSING) { py = R; gy = -R; heading = -CN_PI / 2; }
-        else { py = -R + 2; gy = R + 2; heading = CN_PI / 2; v_pref = 0.3; }
-    } break;
-    default: {
-        const double min_x = -(R + robot_radius + agent_radius), max_x = -(R - robot_radius - agent_radius);
-        const double hx = (max_x - min_x) * mt_dbl(w, q) + min_x;
-        px = hx; gx = -hx; py = 0; gy = 0;
-    } break;
-    }
-    vp = v_pref;
-}
-
-struct Env1 {  // one env's agents in LDS (kernel B)
-    double rpx, rpy, rgx, rgy, rr;
-    double *hpx, *hpy, *hgx, *hgy, *hr, *hvp, *hth;  // [N]
-};
-
-// goal candidate rejection test against the robot and all other humans (positions AND goals)
-__device__ inline bool goal_collides(const cn_config &c, const Env1 &en, int N, int self, double gx, double gy)
-{
-    for (int a = -1; a < N; ++a) {
-        if (a == self) continue;
-        double ax, ay, agx, agy, ar;
-        if (a < 0) { ax = en.rpx; ay = en.rpy; agx = en.rgx; agy = en.rgy; ar = en.rr; }
-        else { ax = en.hpx[a]; ay = en.hpy[a]; agx = en.hgx[a]; agy = en.hgy[a]; ar = en.hr[a]; }
-        const double md = en.hr[self] + ar + c.discomfort_dist;
-        if (np_norm2(gx - ax, gy - ay) < md || np_norm2(gx - agx, gy - agy) < md) return true;
-    }
-    return false;
-}
-
-// Speculative rejection loop: try t = t0 + lane is evaluated by `eval(q, ok)` on the words starting
-// at q = p + W*lane; the first accepted try wins (RVO/reference order), bounded by max_tries (the
-// reference loops forever; after max_tries the last try is accepted and `overflow` is counted).
-// Returns the winning lane of the final round; the caller reads that lane's candidate from LDS.
-template <typename F>
-__device__ int wave_reject(WRng &m, int W, int max_tries, uint32_t &ovf, F eval)
-{
-    const int J = min(64, CN_MT_N / W);
-    for (int t0 = 0;; t0 += J) {
-        m.ensure(W * J);
-        const bool valid = m.lane < J && t0 + m.lane < max_tries;
-        bool ok = false;
-        if (valid) eval(m.p + W * m.lane, ok);
-        const unsigned long long mask = __ballot(valid && ok);
-        if (mask) {
-            const int first = __ffsll((long long)mask) - 1;
-            m.p += W * (first + 1);
-            return first;
-        }
-        if (t0 + J >= max_tries) {
-            const int last = max_tries - 1 - t0;
-            m.p += W * (last + 1);
-            ++ovf;
-            return last;
-        }
-        m.p += W * J;
-    }
-}
-
-__global__ void __launch_bounds__(64) cn_rng_kernel(RngArgs g, cn_config c)
+// cn_reset: CrowdSimDict.reset of every env, one wave (single-wave workgroup) per env
+__global__ void __launch_bounds__(64) cn_reset_kernel(RngArgs g, cn_config c)
 {
     __shared__ uint32_t mtw[2 * CN_MT_N];
     __shared__ double hbuf[7][32];
-    const cn_state_ptrs &S = g.s;
+    __shared__ double slots[6 * 64];
     const int lane = threadIdx.x;
-    const int N = c.human_num;
-    const uint32_t nwork = g.reset_all ? (uint32_t)g.E : *g.work_count;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && g.next_work_count) *g.next_work_count = 0u;
-    for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
-        const uint32_t item = g.reset_all ? (w | 0x80000000u) : g.work[w];
-        const int64_t e = item & 0x7fffffffu;
-        const bool done = (item >> 31) != 0;
-        STAMP_B(w, 0);
+    for (int64_t e = blockIdx.x; e < g.E; e += gridDim.x) {
         Env1 en;
         en.hpx = hbuf[0]; en.hpy = hbuf[1]; en.hgx = hbuf[2]; en.hgy = hbuf[3]; en.hr = hbuf[4]; en.hvp = hbuf[5];
         en.hth = hbuf[6];
-        const int64_t hb = e * N;
         WRng m;
-        m.w = mtw; m.have1 = false; m.slid = false; m.lane = lane;
-        uint32_t ovf = 0;
-        if (!done) {
-            // ---------------- goal changes (crowd_sim_dict.py:260-269) ----------------
-            for (int k = lane; k < CN_MT_N; k += 64) mtw[k] = S.mt[e * CN_MT_N + k];
-            if (lane < N) {
-                en.hpx[lane] = S.h_px[hb + lane]; en.hpy[lane] = S.h_py[hb + lane];
-                en.hgx[lane] = S.h_gx[hb + lane]; en.hgy[lane] = S.h_gy[hb + lane];
-                en.hr[lane] = S.h_r[hb + lane]; en.hvp[lane] = S.h_vpref[hb + lane];
-            }
-            m.p = S.mt_pos[e];
-            ovf = S.overflow[e];
-            en.rpx = S.r_px[e]; en.rpy = S.r_py[e]; en.rgx = S.r_gx[e]; en.rgy = S.r_gy[e]; en.rr = S.r_radius[e];
-            const int sc = S.scenario[e];
-            const bool rgoal = c.random_goal_changing && np_mod(S.gtime[e], 5.0) == 0.0;
-            __syncthreads();
-            STAMP_B(w, 1);
-            if (rgoal) {
-                // update_human_goals_randomly (crowd_sim.py:724-766): U, then tries of (angle, gx_n, gy_n)
-                for (int i = 0; i < N; ++i) {
-                    if (en.hvp[i] == 0) continue;
-                    if (m.rnd() <= c.goal_change_chance) {
-                        const double vp = en.hvp[i] == 0 ? 1.0 : en.hvp[i];
-                        wave_reject(m, 6, c.max_tries, ovf, [&](int q, bool &ok) {
-                            const double angle = mt_dbl(mtw, q) * CN_PI * 2;
-                            const double gxn = (mt_dbl(mtw, q + 2) - 0.5) * vp, gyn = (mt_dbl(mtw, q + 4) - 0.5) * vp;
-                            const double gx = c.circle_radius * cos(angle) + gxn;
-                            const double gy = c.circle_radius * sin(angle) + gyn;
-                            ok = !goal_collides(c, en, N, i, gx, gy);
-                        });
-                        // the accepted try's words end at p: recompute its candidate on every lane
-                        const int q = m.p - 6;
-                        const double angle = mt_dbl(mtw, q) * CN_PI * 2;
-                        const double gxn = (mt_dbl(mtw, q + 2) - 0.5) * vp, gyn = (mt_dbl(mtw, q + 4) - 0.5) * vp;
-                        __syncthreads();
-                        if (lane == 0) {
-                            en.hgx[i] = c.circle_radius * cos(angle) + gxn;
-                            en.hgy[i] = c.circle_radius * sin(angle) + gyn;
-                        }
-                        __syncthreads();
-                    }
-                }
-            }
-            if (c.end_goal_changing) {
-                // update_human_goal (crowd_sim.py:769-811) for humans within radius of their goal
-                for (int i = 0; i < N; ++i) {
-                    if (!(np_norm2(en.hgx[i] - en.hpx[i], en.hgy[i] - en.hpy[i]) < en.hr[i])) continue;
-                    if (m.rnd() <= c.end_goal_change_chance) {
-                        double r_i = en.hr[i], vp_i = en.hvp[i];
-                        if (c.random_radii) r_i += m.unif(-0.1, 0.1);
-                        if (c.random_v_pref) vp_i += m.unif(-0.1, 0.1);
-                        __syncthreads();
-                        if (lane == 0) { en.hr[i] = r_i; en.hvp[i] = vp_i; }
-                        __syncthreads();
-                        const int W = cand_words(sc);
-                        wave_reject(m, W, c.max_tries, ovf, [&](int q, bool &ok) {
-                            double px, py, gx, gy, hd, vp;
-                            cand_attributes(c, mtw, q, sc, vp_i, r_i, en.rr, px, py, gx, gy, hd, vp);
-                            ok = !goal_collides(c, en, N, i, gx, gy);
-                        });
-                        double px, py, gx, gy, hd, vp;
-                        cand_attributes(c, mtw, m.p - W, sc, vp_i, r_i, en.rr, px, py, gx, gy, hd, vp);
-                        __syncthreads();
-                        if (lane == 0) { en.hgx[i] = gx; en.hgy[i] = gy; }
-                        __syncthreads();
-                    }
-                }
-            }
-            STAMP_B(w, 2);
-            // numpy twists lazily: a stream that consumed exactly the 624 words is (old key, pos 624)
-            const bool in1 = m.p > CN_MT_N;
-            if (lane < N) {
-                S.h_gx[hb + lane] = en.hgx[lane]; S.h_gy[hb + lane] = en.hgy[lane];
-                S.h_r[hb + lane] = en.hr[lane]; S.h_vpref[hb + lane] = en.hvp[lane];
-            }
-            if (in1 || m.slid)
-                for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[(in1 ? CN_MT_N : 0) + k];
-            if (lane == 0) { S.mt_pos[e] = in1 ? m.p - CN_MT_N : m.p; S.overflow[e] = ovf; }
-            __syncthreads();
-            STAMP_B(w, 3);
-            continue;
-        }
-        // ---------------- CrowdSimDict.reset (crowd_sim_dict.py:105-203) ----------------
-        const int64_t gidx = c.env_offset + e;
-        int sc;
-        if (c.scenario_mode == CN_SCMODE_SEQUENTIAL) sc = c.scenarios[S.reset_count[e] % c.num_scenarios];
-        else sc = c.scenarios[gidx % c.num_scenarios];
-        if (lane == 0) {
-            uint32_t seed = (uint32_t)(g.counter_offset + S.case_counter[e] + (c.seed + gidx));
-            for (int k = 0; k < CN_MT_N; ++k) {  // mt19937_seed: sequential Knuth chain
-                mtw[k] = seed;
-                seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(k + 1);
-            }
-        }
-        __syncthreads();
-        STAMP_B(w, 1);
-        m.p = CN_MT_N;   // numpy: pos = 624 after seeding, the first draw runs mt19937_gen
-        const double R = c.circle_radius;
-        en.rr = c.robot_radius;
-        double rth;
-        if (c.kinematics == CN_UNICYCLE) {
-            const double angle = m.unif(0, CN_PI * 2);
-            en.rpx = R * cos(angle); en.rpy = R * sin(angle);
-            wave_reject(m, 4, c.max_tries, ovf, [&](int q, bool &ok) {
-                const double gx = -R + (R - -R) * mt_dbl(mtw, q), gy = -R + (R - -R) * mt_dbl(mtw, q + 2);
-                ok = np_norm2(en.rpx - gx, en.rpy - gy) >= 6;
-            });
-            en.rgx = -R + (R - -R) * mt_dbl(mtw, m.p - 4);
-            en.rgy = -R + (R - -R) * mt_dbl(mtw, m.p - 2);
-            rth = m.unif(0, 2 * CN_PI);
-        } else if (c.social_metrics || c.side_preference) {
-            en.rpx = 0; en.rpy = -R; en.rgx = 0; en.rgy = R; rth = CN_PI / 2;
-        } else {
-            wave_reject(m, 8, c.max_tries, ovf, [&](int q, bool &ok) {
-                const double px = -R + (R - -R) * mt_dbl(mtw, q), py = -R + (R - -R) * mt_dbl(mtw, q + 2);
-                const double gx = -R + (R - -R) * mt_dbl(mtw, q + 4), gy = -R + (R - -R) * mt_dbl(mtw, q + 6);
-                ok = np_norm2(px - gx, py - gy) >= 6;
-            });
-            en.rpx = -R + (R - -R) * mt_dbl(mtw, m.p - 8); en.rpy = -R + (R - -R) * mt_dbl(mtw, m.p - 6);
-            en.rgx = -R + (R - -R) * mt_dbl(mtw, m.p - 4); en.rgy = -R + (R - -R) * mt_dbl(mtw, m.p - 2);
-            rth = CN_PI / 2;
-        }
-        const int W = cand_words(sc);
-        for (int i = 0; i < N; ++i) {
-            double vpref = c.human_vpref, rad = c.human_radius;
-            if (c.randomize_attributes) { vpref = m.unif(0.5, 1.5); rad = m.unif(0.3, 0.5); }
-            wave_reject(m, W, c.max_tries, ovf, [&](int q, bool &ok) {
-                double px, py, gx, gy, hd, vp;
-                cand_attributes(c, mtw, q, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
-                bool collide = false;
-                for (int a = 0; a <= i && !collide; ++a) {
-                    double md, ax, ay;
-                    if (a == 0) {
-                        ax = en.rpx; ay = en.rpy;
-                        md = c.kinematics == CN_UNICYCLE ? R / 2 : rad + en.rr + c.discomfort_dist;
-                    } else {
-                        ax = en.hpx[a - 1]; ay = en.hpy[a - 1];
-                        md = rad + en.hr[a - 1] + c.discomfort_dist;
-                    }
-                    if (np_norm2(px - ax, py - ay) < md) collide = true;
-                }
-                ok = !collide;
-            });
-            double px, py, gx, gy, hd, vp;
-            cand_attributes(c, mtw, m.p - W, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
-            __syncthreads();
-            if (lane == 0) {
-                en.hpx[i] = px; en.hpy[i] = py; en.hgx[i] = gx; en.hgy[i] = gy;
-                en.hth[i] = hd; en.hvp[i] = vp; en.hr[i] = rad;
-            }
-            __syncthreads();
-        }
-        STAMP_B(w, 2);
-        const double rpx = en.rpx, rpy = en.rpy;
-        if (lane < N) {
-            const int64_t h = hb + lane;
-            const double px = en.hpx[lane], py = en.hpy[lane];
-            S.h_px[h] = px; S.h_py[h] = py; S.h_gx[h] = en.hgx[lane]; S.h_gy[h] = en.hgy[lane];
-            S.h_vx[h] = 0.0; S.h_vy[h] = 0.0; S.h_r[h] = en.hr[lane]; S.h_vpref[h] = en.hvp[lane];
-            S.h_theta[h] = en.hth[lane];
-            S.o_r[h] = 0.0f; S.o_vmax[h] = 0.0f; S.o_dmask[h] = 0u;
-            // generate_ob(reset=True): robot velocity is 0 (ints) -> float64 FOV path
-            double fx, fy;
-            if (c.kinematics == CN_HOLONOMIC) fov_dir64(atan2(0.0, 0.0), fx, fy);
-            else fov_dir64(rth, fx, fy);
-            double bpx, bpy, bvx, bvy, br;
-            if (in_fov(fx, fy, rpx, rpy, px, py, c.robot_fov)) { bpx = px; bpy = py; bvx = 0; bvy = 0; br = en.hr[lane]; }
-            else { bpx = 15.0; bpy = 15.0; bvx = 0.0; bvy = 0.0; br = 0.3; }
-            S.b_px[h] = bpx; S.b_py[h] = bpy; S.b_vx[h] = bvx; S.b_vy[h] = bvy; S.b_r[h] = br;
-            g.spatial[h * 2] = (float)(bpx - rpx);
-            g.spatial[h * 2 + 1] = (float)(bpy - rpy);
-        }
-        const int A = N + (c.robot_visible ? 1 : 0);
-        if (A > 10) for (int k = lane; k < N * A; k += 64) S.o_perm[e * N * A + k] = 0;
-        // the key after seeding always advanced: it is block 1 (p > 624) or block 0 after slides
-        const bool in1 = m.p > CN_MT_N;
-        for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[(in1 ? CN_MT_N : 0) + k];
-        if (lane == 0) {
-            S.scenario[e] = (int32_t)sc;
-            S.gtime[e] = 0.0; S.r_dv[e] = 0.0;
-            S.r_px[e] = rpx; S.r_py[e] = rpy; S.r_gx[e] = en.rgx; S.r_gy[e] = en.rgy; S.r_theta[e] = rth;
-            S.r_vx[e] = 0.0; S.r_vy[e] = 0.0; S.r_radius[e] = c.robot_radius; S.r_vpref[e] = c.robot_vpref;
-            S.case_counter[e] = (S.case_counter[e] + c.nenv) % g.case_size;
-            S.potential[e] = -fabs(np_norm2(rpx - en.rgx, rpy - en.rgy));
-            S.reset_count[e] += 1;
-            S.ep_return[e] = 0.0; S.ep_len[e] = 0;
-            S.flags[e] = 0; S.overflow[e] = ovf; S.mt_pos[e] = in1 ? m.p - CN_MT_N : m.p;
-            float *rn = g.robot_node + e * 7;
-            rn[0] = (float)rpx; rn[1] = (float)rpy; rn[2] = (float)c.robot_radius;
-            rn[3] = (float)en.rgx; rn[4] = (float)en.rgy; rn[5] = (float)c.robot_vpref; rn[6] = (float)rth;
-            g.temporal[e * 2] = 0.0f; g.temporal[e * 2 + 1] = 0.0f;
-        }
-        __syncthreads();
-        STAMP_B(w, 4);
+        m.w = mtw; m.lane = lane; m.sl = slots;
+        reset_env(g.o, g.pend, c, g.E, e, g.counter_offset, true, m, en);
     }
 }
 
@@ -1609,7 +1916,13 @@ struct cn_engine {
     int64_t state_bytes;
     cn_state_ptrs s;
     uint32_t *work;       // [E]
-    uint32_t *work_count; // [4]
+    uint32_t *work_count; // [16]: [2..4] spawn-list counters (triple buffered)
+    uint32_t *plist;      // [3][E] envs whose next spawn kernel A draws
+    void *pend_mem;       // pending next-episode spawns (PendPtrs)
+    PendPtrs pend;
+    int pend_all;         // next kernel A draws every env's spawn (after cn_reset / cn_set_state)
+    int pend_blocks;      // spare workgroups of kernel A running spawn waves
+    int a_lds;            // kernel A dynamic LDS: max(step plan, spawn waves)
     int64_t case_size, counter_offset;
     int rng_grid;
     uint64_t nstep;
@@ -1708,28 +2021,57 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     default: g->case_size = cfg->test_size; g->counter_offset = 1000; break;
     }
     if (g->case_size <= 0) { delete g; return set_err(CN_EINVAL, "case size (val_size/test_size) must be > 0"); }
+    const int64_t E = g->E, EN = (int64_t)g->E * g->N;
+    auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
+    const int64_t pb_mt = al(E * CN_MT_N * 4), pb_i = al(E * 4), pb_cc = al(E * 8), pb_r = al(5 * E * 8),
+                  pb_h = al(7 * EN * 8);
+    const int64_t pend_bytes = pb_mt + 5 * pb_i + pb_cc + pb_r + pb_h;
     hipError_t e1 = hipMalloc(&g->state, g->state_bytes);
     hipError_t e2 = hipMalloc(&g->work, sizeof(uint32_t) * (g->E + 64));
     hipError_t e3 = hipMalloc(&g->work_count, 64);
-    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
-        hipFree(g->state); hipFree(g->work); hipFree(g->work_count);
+    hipError_t e4 = hipMalloc(&g->plist, sizeof(uint32_t) * 3 * (g->E + 64));
+    hipError_t e5 = hipMalloc(&g->pend_mem, pend_bytes);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
+        hipFree(g->state); hipFree(g->work); hipFree(g->work_count); hipFree(g->plist); hipFree(g->pend_mem);
         delete g;
         return set_err(CN_ENOMEM, "hipMalloc failed");
     }
     hipMemset(g->state, 0, g->state_bytes);
     hipMemset(g->work_count, 0, 64);
+    hipMemset(g->pend_mem, 0, pend_bytes);
+    {
+        char *b = (char *)g->pend_mem;
+        g->pend.mt = (uint32_t *)b; b += pb_mt;
+        g->pend.pos = (int32_t *)b; b += pb_i;
+        g->pend.ovf = (uint32_t *)b; b += pb_i;
+        g->pend.sc = (int32_t *)b; b += pb_i;
+        g->pend.rc = (int32_t *)b; b += pb_i;
+        g->pend.ok = (uint32_t *)b; b += pb_i;
+        g->pend.cc = (int64_t *)b; b += pb_cc;
+        g->pend.r = (double *)b; b += pb_r;
+        g->pend.h = (double *)b;
+    }
+    g->pend_all = 1;
+    {
+        const int nw = g->plan.T / 64;
+        const int64_t need = (E + nw - 1) / nw;
+        g->pend_blocks = (int)(need < 64 ? need : 64);
+        // one RNG region per wave for phase 5, laid over the ORCA scratch (lines, projections, kd order)
+        const int lds_need = g->plan.o_lines + nw * CN_PEND_LDS;
+        g->a_lds = g->plan.total > lds_need ? g->plan.total : lds_need;
+    }
     cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
     // unit-circle table of GEOS's 64-gon point buffer (norm zones)
     double cs[64], sn[64];
     for (int k = 0; k < 64; ++k) { const double a = -(k * (CN_PI / 2 / 16)); cs[k] = cos(a); sn[k] = sin(a); }
     hipMemcpyToSymbol(HIP_SYMBOL(c_circ_cos), cs, sizeof cs);
     hipMemcpyToSymbol(HIP_SYMBOL(c_circ_sin), sn, sizeof sn);
-    if (g->plan.total > 160 * 1024) { cn_destroy(g); return set_err(CN_EUNSUPPORTED, "LDS plan exceeds 160 KiB"); }
-    if (g->plan.total > 64 * 1024) {
+    if (g->a_lds > 160 * 1024) { cn_destroy(g); return set_err(CN_EUNSUPPORTED, "LDS plan exceeds 160 KiB"); }
+    if (g->a_lds > 64 * 1024) {
         (void)hipFuncSetAttribute((const void *)cn_step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  g->plan.total);
+                                  g->a_lds);
         (void)hipFuncSetAttribute((const void *)cn_step_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  g->plan.total);
+                                  g->a_lds);
     }
     g->rng_grid = g->E < 2048 ? g->E : 2048;
     HIPCHK(hipDeviceSynchronize());
@@ -1785,6 +2127,8 @@ void cn_destroy(cn_engine *g)
     hipFree(g->state);
     hipFree(g->work);
     hipFree(g->work_count);
+    hipFree(g->plist);
+    hipFree(g->pend_mem);
     delete g;
 }
 
@@ -1793,12 +2137,12 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     if (!g || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
     RngArgs a;
-    a.s = g->s; a.work = g->work; a.work_count = g->work_count; a.next_work_count = nullptr; a.reset_all = 1;
-    a.E = g->E;
-    a.case_size = g->case_size; a.counter_offset = g->counter_offset;
-    a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
-    hipLaunchKernelGGL(cn_rng_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
+    a.o.s = g->s; a.o.robot_node = robot_node; a.o.temporal = temporal; a.o.spatial = spatial;
+    a.o.case_size = g->case_size;
+    a.pend = g->pend; a.E = g->E; a.counter_offset = g->counter_offset;
+    hipLaunchKernelGGL(cn_reset_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
     HIPCHK(hipGetLastError());
+    g->pend_all = 1;   // every env starts a new episode: draw all next spawns in the next kernel A
     return CN_OK;
 }
 
@@ -1807,29 +2151,32 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
 {
     if (!g || !actions || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    uint32_t *cnt = g->work_count + (g->nstep & 1);        // zeroed by the previous step's kernel B
-    uint32_t *cnt_next = g->work_count + ((g->nstep + 1) & 1);
+    // spawn lists, triple-buffered: launch t appends to t%3, reads (t-1)%3, zeroes (t+1)%3
+    const int kw = (int)(g->nstep % 3), kr = (int)((g->nstep + 2) % 3), kz = (int)((g->nstep + 1) % 3);
     ++g->nstep;
     const bool prof = g->prof_on && g->prof_n < g->prof_cap;
     if (prof) HIPCHK(hipEventRecord(g->ev[3 * g->prof_n], st));
     StepArgs a;
     a.s = g->s; a.actions = actions; a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
     a.reward = reward; a.done = done; a.event = event; a.info = info; a.ep_return = ep_return; a.ep_len = ep_len;
-    a.work = g->work; a.work_count = cnt; a.E = g->E;
+    a.E = g->E;
+    a.case_size = g->case_size;
+    a.plist_w = g->plist + (int64_t)kw * (g->E + 64);
+    a.pcount_w = g->work_count + 2 + kw;
+    a.pcount_zero = g->work_count + 2 + kz;
     const int blocks = (g->E + g->plan.EPB - 1) / g->plan.EPB;
+    a.pend.P = g->pend; a.pend.list = g->plist + (int64_t)kr * (g->E + 64); a.pend.count = g->work_count + 2 + kr;
+    a.pend.all = g->pend_all;
+    a.pend.step_blocks = blocks; a.pend.pend_blocks = g->pend_blocks; a.pend.counter_offset = g->counter_offset;
+    g->pend_all = 0;
+    const int grid = blocks + g->pend_blocks;
     if (g->plan.kd)
-        hipLaunchKernelGGL(cn_step_kernel<true>, dim3(blocks), dim3(g->plan.T), g->plan.total, st, a, g->c);
+        hipLaunchKernelGGL(cn_step_kernel<true>, dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
     else
-        hipLaunchKernelGGL(cn_step_kernel<false>, dim3(blocks), dim3(g->plan.T), g->plan.total, st, a, g->c);
-    HIPCHK(hipGetLastError());
-    if (prof) HIPCHK(hipEventRecord(g->ev[3 * g->prof_n + 1], st));
-    RngArgs b;
-    b.s = g->s; b.work = g->work; b.work_count = cnt; b.next_work_count = cnt_next; b.reset_all = 0; b.E = g->E;
-    b.case_size = g->case_size; b.counter_offset = g->counter_offset;
-    b.robot_node = robot_node; b.temporal = temporal; b.spatial = spatial;
-    hipLaunchKernelGGL(cn_rng_kernel, dim3(g->rng_grid), dim3(64), 0, st, b, g->c);
+        hipLaunchKernelGGL(cn_step_kernel<false>, dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
     HIPCHK(hipGetLastError());
     if (prof) {
+        HIPCHK(hipEventRecord(g->ev[3 * g->prof_n + 1], st));
         HIPCHK(hipEventRecord(g->ev[3 * g->prof_n + 2], st));
         ++g->prof_n;
     }
@@ -1868,6 +2215,7 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
     } else {
         HIPCHK(hipMemcpyAsync(g->state, src, g->state_bytes, hipMemcpyDeviceToDevice, st));
     }
+    g->pend_all = 1;   // pending spawns are keyed by (case_counter, reset_count); redraw them for the new state
     return CN_OK;
 }
 

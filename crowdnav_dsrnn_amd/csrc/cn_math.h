@@ -22,6 +22,18 @@ __device__ __forceinline__ float fdiv(float a, float b) { return a / b; }
 
 // np.linalg.norm of a float64 2-vector: sqrt(fma(b, b, a*a))  (OpenBLAS ddot tail loop is fused)
 __device__ __forceinline__ double np_norm2(double a, double b) { return dsqrt(__fma_rn(b, b, a * a)); }
+// np.linalg.norm((a, b)) < md, exactly, without the square root except within ~2^-48 of the boundary:
+// rn(sqrt(x)) < md  <=>  x < md^2 away from equality (numerics).
+__device__ __forceinline__ bool norm_lt(double a, double b, double md)
+{
+    const double x = __fma_rn(b, b, a * a);
+    if (md > 0) {
+        const double t = md * md;
+        if (x < t * (1.0 - 0x1p-48)) return true;
+        if (x > t * (1.0 + 0x1p-48)) return false;
+    }
+    return dsqrt(x) < md;
+}
 // np.linalg.norm of a float32 2-vector: plain float32
 __device__ __forceinline__ float np_norm2f(float a, float b) { return fsqrt(a * a + b * b); }
 // np.dot of float64 2-vectors

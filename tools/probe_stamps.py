@@ -15,7 +15,7 @@ from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config  # no
 from crowdnav_dsrnn_amd.engine import CrowdNavEngine  # noqa: E402
 
 
-def run(variant, E=4096, N=10, steps=60):
+def run(variant, E=4096, N=10, steps=300):
     c = clone_config(Config())
     c.sim.human_num = N
     c.sim.train_val_sim = ["circle_crossing"]
@@ -43,31 +43,38 @@ def run(variant, E=4096, N=10, steps=60):
     L.cn_debug_stamps(a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p))
     blocks = (E + (256 // N) - 1) // (256 // N)
     A = a.reshape(-1, 8)[:blocks].astype(np.int64)
-    d = np.diff(A[:, :6], axis=1)
+    d = np.diff(A[:, :7], axis=1)
     print("[%s] kernel A avg %.1f us, kernel B avg %.1f us over %d steps" % (variant, ta.value * 1e3 / n.value,
                                                                           tb.value * 1e3 / n.value, n.value))
-    names = ["load", "visibility", "policy+reward terms", "reward ladder", "kinematics+obs+worklist"]
-    tot = (A[:, 5] - A[:, 0])
+    names = ["load", "visibility", "policy+reward terms", "reward ladder", "kinematics+obs", "rng work (phase 5)"]
+    tot = (A[:, 6] - A[:, 0])
     print("  kernel A cycles per workgroup (last step): total median %d max %d" % (np.median(tot), tot.max()))
     for k, nm in enumerate(names):
         print("    %-26s median %8d  max %8d  (%.0f%%)" % (nm, np.median(d[:, k]), d[:, k].max(),
                                                             100 * np.median(d[:, k]) / np.median(tot)))
-    cnt = int(eng.done.sum().item())
-    B = b.reshape(-1, 8).astype(np.int64)
-    used = B[:, 0] > 0
-    Bu = B[used]
-    # items: reset items have stamp 4 set; goal items stop at 3
-    res = Bu[Bu[:, 4] > 0]
-    goal = Bu[Bu[:, 4] == 0]
+    B = b.reshape(-1, 8).astype(np.int64)[:E]
+    t0 = A[:, 0].min()
+    cur = B[:, 0] >= t0                      # items of the last step only
+    res = B[cur & (B[:, 5] >= B[:, 0])]
+    goal = B[cur & (B[:, 4] >= B[:, 0]) & (B[:, 5] < B[:, 0])]
     if len(res):
-        r = np.diff(res[:, :5], axis=1)
-        print("  kernel B reset items (cumulative over run, %d): seed %d  twist %d  spawn %d  write %d  (median cycles)" % (
-            len(res), *np.median(r, axis=0)))
-        print("     reset total max %d" % (res[:, 4] - res[:, 0]).max())
+        r = res[:, 5] - res[:, 0]
+        print("  phase-5 resets (last step, %d envs): cycles median %d p90 %d max %d" % (len(res), np.median(r), np.percentile(r, 90), r.max()))
     if len(goal):
-        gg = np.diff(goal[:, :4], axis=1)
-        print("  kernel B goal items (%d): load %d  lane0 %d  write %d (median cycles); lane0 max %d" % (
-            len(goal), *np.median(gg, axis=0), gg[:, 1].max()))
+        gg = np.diff(goal[:, :5], axis=1)
+        tot = goal[:, 4] - goal[:, 0]
+        print("  phase-5 goal items (last step, %d envs): mt load %d  random %d  end %d  write %d (median); total median %d p90 %d max %d"
+              % (len(goal), *np.median(gg, axis=0), np.median(tot), np.percentile(tot, 90), tot.max()))
+        for slot, nm in ((6, "random"), (7, "end")):
+            v = goal[:, slot]
+            rounds, chg, elig = v // 1000, (v % 1000) // 100, v % 100
+            part = gg[:, 1] if slot == 6 else gg[:, 2]
+            print("     %s pass: eligible mean %.2f, rounds mean %.2f max %d, changes (1st round) mean %.2f" % (
+                nm, elig.mean(), rounds.mean(), rounds.max(), chg.mean()))
+            for r in range(int(rounds.max()) + 1):
+                sel = rounds == r
+                if sel.any():
+                    print("        %d rounds: %4d envs, cycles median %d max %d" % (r, sel.sum(), np.median(part[sel]), part[sel].max()))
     eng.close()
 
 
