@@ -115,6 +115,10 @@ enum { H_PX, H_PY, H_GX, H_GY, H_VX, H_VY, H_R, H_VP, H_TH };
 
 // ------------------------------------------------------------------------------------------------
 // FOV (CrowdSim.detect_visible, crowd_sim.py:820-847)
+// With fov >= 2*pi (the reference default, FOV = 2) the arccos test always passes: an agent is visible
+// iff the normalised dot product is not NaN. Away from under/overflow of |v|^2 that is "heading finite
+// and the agents not coincident", decided without atan2/cos/sin/sqrt/division; `vis360` returns -1
+// where the full computation must decide (|v|^2 outside [1e-300, 1e300]).
 // ------------------------------------------------------------------------------------------------
 // unit FOV direction of an agent with float64 heading
 __device__ inline void fov_dir64(double th, double &fx, double &fy)
@@ -129,6 +133,13 @@ __device__ inline void fov_dir32(float th, double &fx, double &fy)
     float cx = np_cosf(th), cy = np_sinf(th);
     const float nf = np_norm2f(cx, cy);
     fx = (double)fdiv(cx, nf); fy = (double)fdiv(cy, nf);
+}
+__device__ __forceinline__ int vis360(bool heading_finite, double px1, double py1, double px2, double py2)
+{
+    if (!heading_finite) return 0;
+    const double dx = px2 - px1, dy = py2 - py1;
+    const double n2 = __fma_rn(dy, dy, dx * dx);
+    return (n2 > 1e-300 && n2 < 1e300) ? 1 : -1;
 }
 __device__ inline bool in_fov(double fx, double fy, double px1, double py1, double px2, double py2, double fov)
 {
@@ -835,7 +846,13 @@ __device__ __forceinline__ void write_pending(const PendPtrs &P, const cn_config
                               int sc, uint32_t ovf, const uint32_t *mt_src, int pos, int64_t cc, int32_t rc, int lane)
 {
     const int N = c.human_num;
-    for (int k = lane; k < CN_MT_N; k += 64) P.mt[e * CN_MT_N + k] = mt_src[k];
+    {
+        uint32_t v[(CN_MT_N + 63) / 64];
+#pragma unroll
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; v[j] = k < CN_MT_N ? mt_src[k] : 0u; }
+#pragma unroll
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; if (k < CN_MT_N) P.mt[e * CN_MT_N + k] = v[j]; }
+    }
     if (lane < N) {
         const int64_t h = e * N + lane, EN = E * N;
         P.h[h] = en.hpx[lane]; P.h[EN + h] = en.hpy[lane]; P.h[2 * EN + h] = en.hgx[lane];
@@ -866,11 +883,15 @@ __device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &
         S.h_theta[h] = en.hth[lane];
         S.o_r[h] = 0.0f; S.o_vmax[h] = 0.0f; S.o_dmask[h] = 0u;
         // generate_ob(reset=True): robot velocity is 0 (ints) -> float64 FOV path
-        double fx, fy;
-        if (c.kinematics == CN_HOLONOMIC) fov_dir64(atan2(0.0, 0.0), fx, fy);
-        else fov_dir64(rth, fx, fy);
+        const double th0 = c.kinematics == CN_HOLONOMIC ? 0.0 : rth;   // atan2(0, 0) = 0
+        int v = c.robot_fov >= 2.0 * CN_PI ? vis360(isfinite(th0), rpx, rpy, px, py) : -1;
+        if (v < 0) {
+            double fx, fy;
+            fov_dir64(c.kinematics == CN_HOLONOMIC ? atan2(0.0, 0.0) : rth, fx, fy);
+            v = in_fov(fx, fy, rpx, rpy, px, py, c.robot_fov) ? 1 : 0;
+        }
         double bpx, bpy, bvx, bvy, br;
-        if (in_fov(fx, fy, rpx, rpy, px, py, c.robot_fov)) { bpx = px; bpy = py; bvx = 0; bvy = 0; br = en.hr[lane]; }
+        if (v) { bpx = px; bpy = py; bvx = 0; bvy = 0; br = en.hr[lane]; }
         else { bpx = 15.0; bpy = 15.0; bvx = 0.0; bvy = 0.0; br = 0.3; }
         S.b_px[h] = bpx; S.b_py[h] = bpy; S.b_vx[h] = bvx; S.b_vy[h] = bvy; S.b_r[h] = br;
         g.spatial[h * 2] = (float)(bpx - rpx);
@@ -878,7 +899,13 @@ __device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &
     }
     const int A = N + (c.robot_visible ? 1 : 0);
     if (A > 10) for (int k = lane; k < N * A; k += 64) S.o_perm[e * N * A + k] = 0;
-    for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mt_src[k];
+    {   // all loads first, then all stores: mt_src may be LDS or global, so the compiler cannot pipeline
+        uint32_t v[(CN_MT_N + 63) / 64];
+#pragma unroll
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; v[j] = k < CN_MT_N ? mt_src[k] : 0u; }
+#pragma unroll
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; if (k < CN_MT_N) S.mt[e * CN_MT_N + k] = v[j]; }
+    }
     if (lane == 0) {
         S.scenario[e] = (int32_t)sc;
         S.gtime[e] = 0.0; S.r_dv[e] = 0.0;
@@ -1074,7 +1101,13 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
     const int lane = m.lane;
     uint32_t *mtw = m.w;
     const int64_t hb = e * N;
-    for (int k = lane; k < CN_MT_N; k += 64) mtw[k] = S.mt[e * CN_MT_N + k];
+    {
+        uint32_t v[(CN_MT_N + 63) / 64];
+#pragma unroll
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; v[j] = k < CN_MT_N ? S.mt[e * CN_MT_N + k] : 0u; }
+#pragma unroll
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; if (k < CN_MT_N) mtw[k] = v[j]; }
+    }
     m.p = S.mt_pos[e];
     m.have1 = false; m.slid = false;
     uint32_t ovf = S.overflow[e];
@@ -1287,7 +1320,14 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
     STAMP_A(0);
     // ---- phase 0: load state into LDS -----------------------------------------------------------
     double bpx = 0, bpy = 0, bvx = 0, bvy = 0, br = 0;
+    // values needed in later phases are loaded here, so their latency overlaps phase 0
+    float pre_or = 0.0f, pre_vmax = 0.0f;
+    uint32_t pre_dm = 0u;
+    double pre_lax = 0, pre_lay = 0, pre_epr = 0;
+    int32_t pre_epl = 0, pre_sc = 0;
+    uint32_t pre_ovf = 0;
     if (hl) {
+        pre_or = S.o_r[gh]; pre_vmax = S.o_vmax[gh]; pre_dm = S.o_dmask[gh];
         HF(sl, H_PX, tid) = S.h_px[gh]; HF(sl, H_PY, tid) = S.h_py[gh];
         HF(sl, H_GX, tid) = S.h_gx[gh]; HF(sl, H_GY, tid) = S.h_gy[gh];
         HF(sl, H_VX, tid) = S.h_vx[gh]; HF(sl, H_VY, tid) = S.h_vy[gh];
@@ -1303,6 +1343,8 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         RF(sl, R_VP, tid, EPB) = S.r_vpref[ge]; RF(sl, R_POT, tid, EPB) = S.potential[ge];
         RF(sl, R_GT, tid, EPB) = S.gtime[ge]; RF(sl, R_DV, tid, EPB) = S.r_dv[ge];
         sl.rflag[tid] = S.flags[ge];
+        pre_lax = S.last_ax[ge]; pre_lay = S.last_ay[ge]; pre_epr = S.ep_return[ge]; pre_epl = S.ep_len[ge];
+        pre_sc = S.scenario[ge]; pre_ovf = S.overflow[ge];
         // ---- SRNN.clip_action (srnn.py:18-48) + unicycle integrator (crowd_sim_dict.py:211-217)
         float a0 = g.actions[ge * 2], a1 = g.actions[ge * 2 + 1];
         if (holo) {
@@ -1336,22 +1378,39 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
     bool frozen = true;
     if (hl) {
         const int eb = el * N;
-        double fx, fy;
-        if (holo) fov_dir64(atan2(HF(sl, H_VY, tid), HF(sl, H_VX, tid)), fx, fy);
-        else fov_dir64(HF(sl, H_TH, tid), fx, fy);
+        double fx = 0, fy = 0;
+        bool have_dir = false;
+        auto dir = [&]() {
+            if (!have_dir) {
+                if (holo) fov_dir64(atan2(HF(sl, H_VY, tid), HF(sl, H_VX, tid)), fx, fy);
+                else fov_dir64(HF(sl, H_TH, tid), fx, fy);
+                have_dir = true;
+            }
+        };
+        const bool full = c.human_fov >= 2.0 * CN_PI;
+        const bool hfin = holo ? (HF(sl, H_VX, tid) == HF(sl, H_VX, tid) && HF(sl, H_VY, tid) == HF(sl, H_VY, tid))
+                               : isfinite(HF(sl, H_TH, tid));
         const double px = HF(sl, H_PX, tid), py = HF(sl, H_PY, tid);
         for (int k = 0; k < N - 1; ++k) {
             const int j = eb + (k < i ? k : k + 1);
-            if (in_fov(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov)) vis |= 1u << k;
+            int v = full ? vis360(hfin, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j)) : -1;
+            if (v < 0) { dir(); v = in_fov(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov) ? 1 : 0; }
+            if (v) vis |= 1u << k;
         }
-        if (c.robot_visible && in_fov(fx, fy, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB), c.human_fov))
-            vis |= 1u << (N - 1);
+        if (c.robot_visible) {
+            int v = full ? vis360(hfin, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB)) : -1;
+            if (v < 0) {
+                dir();
+                v = in_fov(fx, fy, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB), c.human_fov) ? 1 : 0;
+            }
+            if (v) vis |= 1u << (N - 1);
+        }
         if (orca) {
             frozen = (sl.rflag[el] & CN_FLAG_ORCA_FROZEN) != 0;
             if (frozen) {
-                sl.orad[tid] = S.o_r[gh];
-                my_vmax = S.o_vmax[gh];
-                dm = S.o_dmask[gh];
+                sl.orad[tid] = pre_or;
+                my_vmax = pre_vmax;
+                dm = pre_dm;
             } else {  // first ORCA.predict of the episode creates the simulator (orca.py:85-109)
                 sl.orad[tid] = (float)(HF(sl, H_R, tid) + 0.01 + c.orca_safety_space);
                 my_vmax = (float)HF(sl, H_VP, tid);
@@ -1658,7 +1717,7 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         double jerk;
         {
             const float ax = (float)cvx - (float)RF(sl, R_VX, tid, EPB), ay = (float)cvy - (float)RF(sl, R_VY, tid, EPB);
-            const float dax = ax - (float)S.last_ax[ge], day = ay - (float)S.last_ay[ge];
+            const float dax = ax - (float)pre_lax, day = ay - (float)pre_lay;
             jerk = (double)(dax * dax + day * day);
             S.last_ax[ge] = ax; S.last_ay[ge] = ay;
         }
@@ -1699,11 +1758,11 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
             info[CN_INFO_DIST_TO_GOAL] = (float)dist_to_goal;
             info[CN_INFO_SPEED_VIOLATION] = speed > c.max_walking_speed ? 1.0f : 0.0f;
             info[CN_INFO_MIN_DIST] = (float)dmin;
-            info[CN_INFO_SCENARIO] = (float)S.scenario[ge];
+            info[CN_INFO_SCENARIO] = (float)pre_sc;
             info[CN_INFO_SIDE_LEFT] = (float)side_l;
             info[CN_INFO_SIDE_RIGHT] = (float)side_r;
             info[CN_INFO_SEPARATION] = (float)sep;
-            info[CN_INFO_OVERFLOW] = (float)S.overflow[ge];
+            info[CN_INFO_OVERFLOW] = (float)pre_ovf;
         }
         // robot kinematics (agent.py:198-212)
         if (holo) {
@@ -1717,8 +1776,8 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         }
         sl.rflag[tid] = flags | CN_FLAG_ROBOT_F32;
         RF(sl, R_GT, tid, EPB) = gt + dt;
-        const double epr = S.ep_return[ge] + reward;
-        const int32_t epl = S.ep_len[ge] + 1;
+        const double epr = pre_epr + reward;
+        const int32_t epl = pre_epl + 1;
         S.ep_return[ge] = epr; S.ep_len[ge] = epl;
         if (g.reward) g.reward[ge] = (float)reward;
         if (g.done) g.done[ge] = (uint8_t)done;
@@ -1735,11 +1794,17 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         const double npx = HF(sl, H_PX, tid) + nvx * dt, npy = HF(sl, H_PY, tid) + nvy * dt;
         S.h_px[gh] = npx; S.h_py[gh] = npy; S.h_vx[gh] = nvx; S.h_vy[gh] = nvy;
         // detect_visible(robot, human, robot1=True) on the POST-move state (robot velocity now float32)
-        double fx, fy;
-        if (holo) fov_dir32(atan2f((float)RF(sl, R_VY, el, EPB), (float)RF(sl, R_VX, el, EPB)), fx, fy);
-        else fov_dir32((float)RF(sl, R_TH, el, EPB), fx, fy);
         const double rnx = RF(sl, R_NX, el, EPB), rny = RF(sl, R_NY, el, EPB);
-        if (in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov)) {
+        const float rvx = (float)RF(sl, R_VX, el, EPB), rvy = (float)RF(sl, R_VY, el, EPB);
+        const bool rfin = holo ? (rvx == rvx && rvy == rvy) : isfinite((float)RF(sl, R_TH, el, EPB));
+        int rv = c.robot_fov >= 2.0 * CN_PI ? vis360(rfin, rnx, rny, npx, npy) : -1;
+        if (rv < 0) {
+            double fx, fy;
+            if (holo) fov_dir32(atan2f(rvy, rvx), fx, fy);
+            else fov_dir32((float)RF(sl, R_TH, el, EPB), fx, fy);
+            rv = in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov) ? 1 : 0;
+        }
+        if (rv) {
             bpx = npx; bpy = npy; bvx = nvx; bvy = nvy; br = HF(sl, H_R, tid);
         } else {
             bpx = bpx + bvx * dt; bpy = bpy + bvy * dt;
@@ -1784,7 +1849,7 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
         const bool rgoal = c.random_goal_changing && np_mod(gt, 5.0) == 0.0;
         const bool egoal = c.end_goal_changing && endg;
         sl.rflag[EPB + tid] = (done ? 1u : 0u) | (rgoal ? 2u : 0u) | (egoal ? 4u : 0u) |
-                              (S.ep_len[ge] == 1 ? 8u : 0u);
+                              (pre_epl + 1 == 1 ? 8u : 0u);
     }
     __syncthreads();
     STAMP_A(5);
