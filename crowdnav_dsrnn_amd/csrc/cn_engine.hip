@@ -29,7 +29,7 @@ using namespace cn;
 // Diagnostic build only (-DCN_STAMPS): per-workgroup s_memtime stamps at phase boundaries, read back
 // with cn_debug_stamps(). The shipped library is built without it (no stamp executes).
 #ifdef CN_STAMPS
-#define CN_NSTAMP 8
+#define CN_NSTAMP 12
 __device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 #define STAMP_A(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + (k)] = clock64(); } while (0)
@@ -65,7 +65,7 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.A = N + (robot_visible ? 1 : 0);
     p.M = p.A - 1;
     p.kd = p.A > 10;
-    p.T = N > 12 ? 128 : CN_BLK;
+    p.T = N > 12 ? 128 : (p.kd ? CN_BLK : 64);   // register path: one wave per workgroup (no cross-wave barriers)
     p.EPB = p.T / N;
     const int T = p.T;
     const int ML = p.kd ? (p.M > 0 ? p.M : 1) : 0;   // LDS ORCA lines only on the kd-tree path
@@ -1478,11 +1478,14 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
 #if defined(CN_ABL_NO_LP)
                 rx = L[0].x + L[8].y; ry = L[4].z + (float)cnt;   // timing-only ablation build
 #else
+                STAMP_A(7);
                 const int fail_at = lp2_r(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
+                STAMP_A(8);
 #if defined(CN_ABL_NO_LP3)
                 rx += (float)fail_at;                            // timing-only ablation build
 #else
                 if (fail_at < cnt) lp3_r(L, cnt, fail_at, my_vmax, rx, ry);
+                STAMP_A(9);
 #endif
 #endif
             } else {
@@ -2120,7 +2123,8 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     {
         const int nw = g->plan.T / 64;
         const int64_t need = (E + nw - 1) / nw;
-        g->pend_blocks = (int)(need < 64 ? need : 64);
+        const int cap = 256 / nw;
+        g->pend_blocks = (int)(need < cap ? need : cap);
         // one RNG region per wave for phase 5, laid over the ORCA scratch (lines, projections, kd order)
         const int lds_need = g->plan.o_lines + nw * CN_PEND_LDS;
         g->a_lds = g->plan.total > lds_need ? g->plan.total : lds_need;

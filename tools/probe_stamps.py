@@ -29,8 +29,8 @@ def run(variant, E=4096, N=10, steps=300):
     eng.reset()
     L = _lib.lib()
     L.cn_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    a = np.zeros(4096 * 8, np.uint64)
-    b = np.zeros(8192 * 8, np.uint64)
+    a = np.zeros(4096 * 12, np.uint64)
+    b = np.zeros(8192 * 12, np.uint64)
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
     acts = torch.rand((steps, E, 2), generator=g, device="cuda:0") * 0.2 - 0.1
@@ -41,8 +41,9 @@ def run(variant, E=4096, N=10, steps=300):
     ta, tb, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
     L.cn_profile_read(eng._h, ctypes.byref(ta), ctypes.byref(tb), ctypes.byref(n))
     L.cn_debug_stamps(a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p))
-    blocks = (E + (256 // N) - 1) // (256 // N)
-    A = a.reshape(-1, 8)[:blocks].astype(np.int64)
+    T = 64 if N <= 10 else (256 if N <= 12 else 128)
+    blocks = (E + (T // N) - 1) // (T // N)
+    A = a.reshape(-1, 12)[:blocks].astype(np.int64)
     d = np.diff(A[:, :7], axis=1)
     print("[%s] kernel A avg %.1f us, kernel B avg %.1f us over %d steps" % (variant, ta.value * 1e3 / n.value,
                                                                           tb.value * 1e3 / n.value, n.value))
@@ -52,8 +53,11 @@ def run(variant, E=4096, N=10, steps=300):
     for k, nm in enumerate(names):
         print("    %-26s median %8d  max %8d  (%.0f%%)" % (nm, np.median(d[:, k]), d[:, k].max(),
                                                             100 * np.median(d[:, k]) / np.median(tot)))
-    B = b.reshape(-1, 8).astype(np.int64)[:E]
+    B = b.reshape(-1, 12).astype(np.int64)[:E]
     t0 = A[:, 0].min()
+    sub = [("lines+sort", A[:, 7] - A[:, 2]), ("LP2", A[:, 8] - A[:, 7]), ("LP3", A[:, 9] - A[:, 8]), ("VR+terms", A[:, 3] - A[:, 9])]
+    for nm, v in sub:
+        print("      wave0 %-12s median %8d  max %8d" % (nm, np.median(v), v.max()))
     cur = B[:, 0] >= t0                      # items of the last step only
     res = B[cur & (B[:, 5] >= B[:, 0])]
     goal = B[cur & (B[:, 4] >= B[:, 0]) & (B[:, 5] < B[:, 0])]

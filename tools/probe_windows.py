@@ -43,6 +43,35 @@ def main(steps=600, window=50, variant="c2", E=4096, N=10):
     eng.close()
 
 
+def per_step(steps=300, show=60, E=4096, N=10):
+    """Kernel time of each individual step (profile window of 1), to see the goal-change bursts."""
+    c = clone_config(Config())
+    c.sim.human_num = N
+    c.sim.train_val_sim = ["circle_crossing"]
+    c.action_space.kinematics = "unicycle"
+    eng = CrowdNavEngine(make_cn_config(c, num_envs=E), "cuda:0")
+    eng.reset()
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(0)
+    acts = torch.rand((steps, E, 2), generator=g, device="cuda:0") * 0.2 - 0.1
+    L = _lib.lib()
+    ta, tb, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    ts = []
+    for s in range(steps):
+        _lib.check(L.cn_profile(eng._h, 1, 1))
+        eng.step(acts[s])
+        _lib.check(L.cn_profile_read(eng._h, ctypes.byref(ta), ctypes.byref(tb), ctypes.byref(n)))
+        ts.append(ta.value * 1e3)
+    import numpy as np
+    t = np.array(ts[steps - show:])
+    print("per-step kernel us (last %d): %s" % (show, " ".join("%.0f" % x for x in t)))
+    print("median %.1f mean %.1f max %.1f" % (np.median(t), t.mean(), t.max()))
+    eng.close()
+
+
 if __name__ == "__main__":
     a = sys.argv[1:]
+    if a and a[0] == "per_step":
+        per_step()
+        sys.exit(0)
     main(int(a[0]) if a else 600, int(a[1]) if len(a) > 1 else 50, a[2] if len(a) > 2 else "c2")
