@@ -24,6 +24,16 @@
 
 using namespace cn;
 
+// LDS ordering among the lanes of ONE wave (kernel B workgroups are a single wave; the spawn waves of
+// kernel A run independently of the other waves of their workgroup): no s_barrier needed, only the
+// compiler/LDS ordering a release/acquire pair at wavefront scope gives.
+__device__ __forceinline__ void wsync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 #define CN_BLK 256
 
 // Diagnostic build only (-DCN_STAMPS): per-workgroup s_memtime stamps at phase boundaries, read back
@@ -46,16 +56,20 @@ __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 // ------------------------------------------------------------------------------------------------
 struct StepPlan {
     int T;       // threads per workgroup (256; 128 when N > 12 so the kd-tree path's LDS lines fit)
+    int H;       // human-lane stride: 64 on the quad path (humans in wave 0), T on the kd-tree path
     int EPB;     // envs per workgroup
     int M;       // observed slots per human (ORCA lines upper bound)
     int A;       // agents per RVO2 simulator
     int kd;      // A > 10: KdTree ordering needed
     // LDS byte offsets
-    int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_lines, o_proj, o_nd, o_ns, o_perm, total;
+    int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_vis, o_nv, o_lines, o_proj, o_nd, o_ns, o_perm,
+        total;
+    int rng_waves;   // phase-5 RNG regions (CN_PEND_LDS each), laid over o_lines
 };
 
 #define CN_RENV_F 14   // robot/env doubles per env in LDS
 #define CN_HUM_F 9     // human doubles per lane in LDS
+#define CN_PEND_LDS (2 * CN_MT_N * 4 + 7 * 32 * 8 + 6 * 64 * 8)   // per RNG wave: MT ring, agent table, try slots
 
 __host__ __device__ inline int cn_align16(int x) { return (x + 15) & ~15; }
 
@@ -65,24 +79,32 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.A = N + (robot_visible ? 1 : 0);
     p.M = p.A - 1;
     p.kd = p.A > 10;
-    p.T = N > 12 ? 128 : (p.kd ? CN_BLK : 64);   // register path: one wave per workgroup (no cross-wave barriers)
-    p.EPB = p.T / N;
-    const int T = p.T;
-    const int ML = p.kd ? (p.M > 0 ? p.M : 1) : 0;   // LDS ORCA lines only on the kd-tree path
+    // quad path (A <= 10): 4 waves, the humans of EPB envs on wave 0's lanes for the per-human phases,
+    // all 256 lanes (4 per human) for ORCA. kd-tree path: one lane per human throughout.
+    p.T = p.kd ? (N > 12 ? 128 : CN_BLK) : CN_BLK;
+    p.H = p.kd ? p.T : 64;
+    p.EPB = p.H / N;
+    const int H = p.H, T = p.T;
+    const int ML = p.M > 0 ? p.M : 1;
     int o = 0;
     p.o_renv = o;  o = cn_align16(o + CN_RENV_F * p.EPB * 8);
     p.o_racts = o; o = cn_align16(o + 2 * p.EPB * 4);
     p.o_rflag = o; o = cn_align16(o + 2 * p.EPB * 4);
     p.o_rvr = o;   o = cn_align16(o + 8 * p.EPB * 8);
-    p.o_hum = o;   o = cn_align16(o + CN_HUM_F * T * 8);
-    p.o_lane = o;  o = cn_align16(o + T * 8 + T * 4);      // closest distance (f64) + flag word
-    p.o_orad = o;  o = cn_align16(o + T * 4);
-    p.o_lines = o; o = cn_align16(o + ML * T * 16);
-    p.o_proj = o;  o = cn_align16(o + ML * T * 16);
-    p.o_nd = o;    o = cn_align16(o + ML * T * 4);
-    p.o_ns = o;    o = cn_align16(o + ML * T);
+    p.o_hum = o;   o = cn_align16(o + CN_HUM_F * H * 8);
+    p.o_lane = o;  o = cn_align16(o + H * 8 + H * 4);      // closest distance (f64) + flag word
+    p.o_orad = o;  o = cn_align16(o + H * 4);
+    p.o_vis = o;   o = cn_align16(o + 3 * H * 4);          // visible mask, dummy mask, frozen max speed
+    p.o_nv = o;    o = cn_align16(o + H * 16);             // new velocity (double2)
+    // ORCA lines: kd path [M][T] per lane; quad path [H][M] per human (sorted lines, projected lines, distSq)
+    p.o_lines = o; o = cn_align16(o + ML * (p.kd ? T : H) * 16);
+    p.o_proj = o;  o = cn_align16(o + ML * (p.kd ? T : H) * 16);
+    p.o_nd = o;    o = cn_align16(o + ML * (p.kd ? T : H) * 4);
+    p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * T : 0));
     p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * T : 0));
-    p.total = o;
+    p.rng_waves = p.kd ? T / 64 : 2;
+    const int rng_end = p.o_lines + p.rng_waves * CN_PEND_LDS;
+    p.total = o > rng_end ? o : rng_end;
     return p;
 }
 
@@ -97,6 +119,10 @@ struct SL {
     double *cd;       // [T]
     uint32_t *lf;     // [T]
     float *orad;      // [T]
+    uint32_t *vis;    // [H] visible-now mask of the human's observed slots (quad path)
+    uint32_t *dm;     // [H] dummy-at-creation mask
+    float *vmax;      // [H] frozen RVO2 max speed
+    double2 *nv;      // [H] new velocity from the human policy
     float4 *lines;    // [M][T]  (kd-tree path)
     float4 *proj;     // [M][T]  linearProgram3's projected lines (kd-tree path)
     float *nd;        // [M][T]
@@ -507,6 +533,131 @@ __device__ __forceinline__ void lp3_r(const float4 (&L)[RMM], int n, int begin, 
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// ORCA linear programs on a QUAD of lanes per human (A <= 10). The lines live in LDS ([human][M]);
+// every quad-uniform quantity (the result, loop indices, branch conditions) is computed redundantly by
+// the 4 lanes, and the inner loop of linearProgram1 over the earlier lines is split across them: lane s
+// takes lines s, s+4, ... and the quad combines tLeft = max, tRight = min and the parallel-line failure.
+// tLeft only grows and tRight only shrinks in RVO2's sequential loop, and its exits ("tLeft > tRight",
+// "parallel line with numerator < 0") are order independent, so the combined result is RVO2's.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float quad_xor1(float x)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ float quad_xor2(float x)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+}
+__device__ __forceinline__ int quad_xor1i(int x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false); }
+__device__ __forceinline__ int quad_xor2i(int x) { return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false); }
+__device__ __forceinline__ float quad_min(float x)
+{
+    float y = quad_xor1(x); x = y < x ? y : x;
+    y = quad_xor2(x); return y < x ? y : x;
+}
+__device__ __forceinline__ float quad_max(float x)
+{
+    float y = quad_xor1(x); x = x < y ? y : x;
+    y = quad_xor2(x); return x < y ? y : x;
+}
+__device__ __forceinline__ int quad_or(int x)
+{
+    x |= quad_xor1i(x);
+    return x | quad_xor2i(x);
+}
+
+// linearProgram1 on line `no` of Lb (valid lines: bits of vmask), quad-cooperative
+__device__ __forceinline__ bool lp1_q(const float4 *Lb, uint32_t vmask, int no, float radius, int s, float &tL,
+                                      float &tR)
+{
+    const float4 ln = Lb[no];
+    const float dot = ln.x * ln.z + ln.y * ln.w;
+    const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
+    const float sd = fsqrt(disc);
+    float ptl = -INFINITY, ptr = INFINITY;
+    int pf = 0;
+    for (int j = s; j < no; j += 4) {
+        if (!((vmask >> j) & 1u)) continue;
+        const float4 li = Lb[j];
+        const float den = det2(ln.z, ln.w, li.z, li.w);
+        const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
+        const bool par = fabsf(den) <= RVO_EPSILON;
+        if (par && num < 0.0f) pf = 1;
+        const float t = fdiv(num, den);
+        if (!par && den >= 0.0f && t < ptr) ptr = t;
+        if (!par && !(den >= 0.0f) && ptl < t) ptl = t;
+    }
+    ptr = quad_min(ptr);
+    ptl = quad_max(ptl);
+    pf = quad_or(pf);
+    float tr = -dot + sd, tl = -dot - sd;
+    tr = ptr < tr ? ptr : tr;
+    tl = tl < ptl ? ptl : tl;
+    tL = tl; tR = tr;
+    return !(disc < 0.0f || pf || tl > tr);
+}
+
+// linearProgram2 (optimize closest to (ox, oy)); returns the index of the failing line or n
+__device__ __forceinline__ int lp2_q(const float4 *Lb, int n, float radius, float ox, float oy, int s, float &rx,
+                                     float &ry)
+{
+    if (ox * ox + oy * oy > radius * radius) {
+        const float inv = fdiv(1.0f, fsqrt(ox * ox + oy * oy));
+        rx = (ox * inv) * radius; ry = (oy * inv) * radius;
+    } else { rx = ox; ry = oy; }
+    for (int i = 0; i < n; ++i) {
+        const float4 li = Lb[i];
+        if (det2(li.z, li.w, li.x - rx, li.y - ry) > 0.0f) {
+            float tL, tR;
+            if (!lp1_q(Lb, 0xffffffffu, i, radius, s, tL, tR)) return i;
+            const float t = li.z * (ox - li.x) + li.w * (oy - li.y);
+            if (t < tL) { rx = li.x + tL * li.z; ry = li.y + tL * li.w; }
+            else if (t > tR) { rx = li.x + tR * li.z; ry = li.y + tR * li.w; }
+            else { rx = li.x + t * li.z; ry = li.y + t * li.w; }
+        }
+    }
+    return n;
+}
+
+// linearProgram3 from line `begin` (agents only); Pb = the human's projected-line scratch
+__device__ __forceinline__ void lp3_q(const float4 *Lb, float4 *Pb, int n, int begin, float radius, int s, float &rx,
+                                      float &ry)
+{
+    float distance = 0.0f;
+    for (int i = begin; i < n; ++i) {
+        const float4 li = Lb[i];
+        if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
+            int pv = 0;
+            for (int j = s; j < i; j += 4) {
+                bool v;
+                const float4 pj = proj_line(li, Lb[j], v);
+                Pb[j] = pj;
+                if (v) pv |= 1 << j;
+            }
+            pv = quad_or(pv);
+            wsync();
+            const float tx = rx, ty = ry;
+            const float ox = -li.w, oy = li.z;   // linearProgram2(projLines, radius, (-d.y, d.x), true)
+            rx = ox * radius; ry = oy * radius;
+            bool fail = false;
+            for (int k = 0; k < i && !fail; ++k) {
+                if (!((pv >> k) & 1)) continue;
+                const float4 pk = Pb[k];
+                if (det2(pk.z, pk.w, pk.x - rx, pk.y - ry) > 0.0f) {
+                    float tL, tR;
+                    if (!lp1_q(Pb, (uint32_t)pv, k, radius, s, tL, tR)) fail = true;
+                    else if (ox * pk.z + oy * pk.w > 0.0f) { rx = pk.x + tR * pk.z; ry = pk.y + tR * pk.w; }
+                    else { rx = pk.x + tL * pk.z; ry = pk.y + tL * pk.w; }
+                }
+            }
+            if (fail) { rx = tx; ry = ty; }
+            distance = det2(li.z, li.w, li.x - rx, li.y - ry);
+            wsync();
+        }
+    }
+}
+
 // one ORCA line (Agent::computeNewVelocity, agent branch) of self vs another agent
 __device__ __forceinline__ float4 orca_line(float X0, float Y0, float VX0, float VY0, float R0, float ox, float oy,
                                            float ovx, float ovy, float orr, float invTH, float invTS)
@@ -587,15 +738,6 @@ struct RngArgs {   // cn_reset_kernel
     int64_t counter_offset;
 };
 
-// LDS ordering among the lanes of ONE wave (kernel B workgroups are a single wave; the spawn waves of
-// kernel A run independently of the other waves of their workgroup): no s_barrier needed, only the
-// compiler/LDS ordering a release/acquire pair at wavefront scope gives.
-__device__ __forceinline__ void wsync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 // numpy MT19937 stream over a two-block LDS ring: block 0 = current key words, block 1 = the key after
 // the next mt19937_gen. Every lane of the (single-wave) workgroup keeps the same stream position `p`;
@@ -763,7 +905,6 @@ __device__ int wave_reject2(WRng &m, int W, int NA, int max_tries, uint32_t &ovf
     }
 }
 
-#define CN_PEND_LDS (2 * CN_MT_N * 4 + 7 * 32 * 8 + 6 * 64 * 8)   // per RNG wave: MT ring, agent table, try slots
 
 // The random part of CrowdSimDict.reset (crowd_sim_dict.py:110-156; generate_robot_humans,
 // crowd_sim.py:555-663; generate_circle_crossing_human :359-393): reseed the env's stream with
@@ -1172,16 +1313,18 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P, 
 // (or of every env after cn_reset / cn_set_state). One wave per env, independent of the other waves.
 struct PendLaunch {
     PendPtrs P;
-    const uint32_t *list;   // envs reset by the previous kernel B
+    const uint32_t *list;   // envs reset by the previous launch
     const uint32_t *count;
     int all;                // 1: every env (list ignored)
     int step_blocks, pend_blocks;
+    int waves;              // spawning waves per spare workgroup (RNG regions that fit the launch's LDS)
     int64_t counter_offset;
 };
 
 __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_ptrs &S, const cn_config &c, int E, char *smem)
 {
-    const int nw = blockDim.x / 64, w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    const int nw = pl.waves, w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    if (w >= nw) return;
     char *base = smem + w * CN_PEND_LDS;
     uint32_t *mtw = (uint32_t *)base;
     double *hb = (double *)(base + 2 * CN_MT_N * 4);
@@ -1278,7 +1421,7 @@ __device__ inline float bbox_dist(float x, float y, float mnx, float mxx, float 
 }
 
 template <bool KD>
-__global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c)
+__global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g, cn_config c)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if ((int)blockIdx.x >= g.pend.step_blocks) {  // spare workgroups: draw upcoming episodes' spawns
@@ -1290,15 +1433,19 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
     const StepPlan P = cn_step_plan(N, c.robot_visible);
     const int EPB = P.EPB, M = P.M, A = P.A;
     SL sl;
-    sl.T = P.T;
+    sl.T = P.H;
     sl.r = (double *)(smem + P.o_renv);
     sl.act = (float *)(smem + P.o_racts);
     sl.rflag = (uint32_t *)(smem + P.o_rflag);
     sl.rvr = (double *)(smem + P.o_rvr);
     sl.h = (double *)(smem + P.o_hum);
     sl.cd = (double *)(smem + P.o_lane);
-    sl.lf = (uint32_t *)(smem + P.o_lane + P.T * 8);
+    sl.lf = (uint32_t *)(smem + P.o_lane + P.H * 8);
     sl.orad = (float *)(smem + P.o_orad);
+    sl.vis = (uint32_t *)(smem + P.o_vis);
+    sl.dm = sl.vis + P.H;
+    sl.vmax = (float *)(sl.vis + 2 * P.H);
+    sl.nv = (double2 *)(smem + P.o_nv);
     sl.lines = (float4 *)(smem + P.o_lines);
     sl.proj = (float4 *)(smem + P.o_proj);
     sl.nd = (float *)(smem + P.o_nd);
@@ -1420,200 +1567,97 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
                 S.o_dmask[gh] = dm;
             }
         }
+        sl.vis[tid] = vis; sl.dm[tid] = dm; sl.vmax[tid] = my_vmax;
     }
     __syncthreads();
     STAMP_A(2);
 
     // ---- phase 2: human policy (PRE-move state) + per-human reward terms -------------------------
     double nvx = 0.0, nvy = 0.0;
-    if (hl) {
-        const int eb = el * N;
-        const double px = HF(sl, H_PX, tid), py = HF(sl, H_PY, tid);
-        const double vx0 = HF(sl, H_VX, tid), vy0 = HF(sl, H_VY, tid);
-        const double rad = HF(sl, H_R, tid), vpref = HF(sl, H_VP, tid);
+    // per-human terms of calc_reward (crowd_sim.py:934-969), PRE-move, for human lane hh
+    auto reward_terms = [&](int hh) {
+        const int elh = hh / N;
+        const double px = HF(sl, H_PX, hh), py = HF(sl, H_PY, hh);
+        const double vx0 = HF(sl, H_VX, hh), vy0 = HF(sl, H_VY, hh), rad = HF(sl, H_R, hh);
+        const double rdx = px - RF(sl, R_PX, elh, EPB), rdy = py - RF(sl, R_PY, elh, EPB);
+        sl.cd[hh] = dsqrt(rdx * rdx + rdy * rdy) - rad - RF(sl, R_RAD, elh, EPB);
+        double hcx[4], hcy[4], rcx[4], rcy[4];
+        vel_rect(px, py, vx0, vy0, rad, false, hcx, hcy);
+        for (int k = 0; k < 4; ++k) { rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh]; }
+        uint32_t f = quads_intersect(rcx, rcy, hcx, hcy) ? LF_VR : 0u;
+        if (!(np_norm2(px - HF(sl, H_GX, hh), py - HF(sl, H_GY, hh)) < rad)) f |= LF_NOTREACHED;
+        sl.lf[hh] = f;
+    };
+    if constexpr (!KD) {
+        const int nh = nenv_here * N;
         if (orca) {
-            const float rdummy = (float)(c.human_radius + 0.01 + c.orca_safety_space);
-            const float X0 = (float)px, Y0 = (float)py, VX0 = (float)vx0, VY0 = (float)vy0;
-            const float R0 = sl.orad[tid];
-            const float rangeSq = (float)c.orca_neighbor_dist * (float)c.orca_neighbor_dist;
-            const float invTH = fdiv(1.0f, (float)c.orca_time_horizon);
-            const float invTS = fdiv(1.0f, (float)dt);
-            // preferred velocity: unit vector to the goal only if farther than 1 (orca.py:118-122)
-            double gdx = HF(sl, H_GX, tid) - px, gdy = HF(sl, H_GY, tid) - py;
-            const double speed = np_norm2(gdx, gdy);
-            if (speed > 1.0) { gdx = ddiv(gdx, speed); gdy = ddiv(gdy, speed); }
-            float rx, ry;
-            if constexpr (!KD) {
-                // <= 10 agents: the KdTree is one leaf, so the neighbour list is the in-range slots
-                // stably sorted by distSq (Agent::insertAgentNeighbor); lines and sort in registers
-                float4 raw[RMM], L[RMM];
-                float d[RMM];
-                bool inr[RMM];
+            // ORCA.predict for every human (orca.py:64-139), a quad of lanes per human. <= 10 agents: the
+            // KdTree is one leaf, so the neighbour list is the in-range slots stably sorted by distSq
+            // (Agent::insertAgentNeighbor). Lane sq builds the lines of slots sq, sq+4, sq+8.
+            const int h = tid >> 2, sq = tid & 3;
+            if (h < nh) {
+                const int elq = h / N, iq = h - elq * N, eb = elq * N;
+                const uint32_t visq = sl.vis[h], dmq = sl.dm[h];
+                const double px = HF(sl, H_PX, h), py = HF(sl, H_PY, h);
+                const float rdummy = (float)(c.human_radius + 0.01 + c.orca_safety_space);
+                const float X0 = (float)px, Y0 = (float)py;
+                const float VX0 = (float)HF(sl, H_VX, h), VY0 = (float)HF(sl, H_VY, h);
+                const float R0 = sl.orad[h];
+                const float rangeSq = (float)c.orca_neighbor_dist * (float)c.orca_neighbor_dist;
+                const float invTH = fdiv(1.0f, (float)c.orca_time_horizon);
+                const float invTS = fdiv(1.0f, (float)dt);
+                // preferred velocity: unit vector to the goal only if farther than 1 (orca.py:118-122)
+                double gdx = HF(sl, H_GX, h) - px, gdy = HF(sl, H_GY, h) - py;
+                const double speed = np_norm2(gdx, gdy);
+                if (speed > 1.0) { gdx = ddiv(gdx, speed); gdy = ddiv(gdy, speed); }
+                float *D = sl.nd + h * M;
+                float4 *Lb = sl.lines + h * M, *Pb = sl.proj + h * M;
+                uint32_t inm = 0;
+                float4 rawv[3];
+                float dv[3];
 #pragma unroll
-                for (int k = 0; k < RMM; ++k) {
-                    inr[k] = false; d[k] = 0.0f;
-                    raw[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int u = 0; u < 3; ++u) {
+                    const int k = sq + 4 * u;
+                    rawv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    dv[u] = 0.0f;
                     if (k < M) {
                         float x, y, vx, vy, r;
-                        slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, x, y, vx, vy, r);
+                        slot_agent(sl, c, eb, elq, EPB, N, iq, k, visq, dmq, rdummy, x, y, vx, vy, r);
                         const float dx = X0 - x, dy = Y0 - y;
-                        d[k] = dx * dx + dy * dy;
-                        inr[k] = d[k] < rangeSq;
-                        raw[k] = orca_line(X0, Y0, VX0, VY0, R0, x, y, vx, vy, r, invTH, invTS);
+                        dv[u] = dx * dx + dy * dy;
+                        if (dv[u] < rangeSq) inm |= 1u << k;
+                        rawv[u] = orca_line(X0, Y0, VX0, VY0, R0, x, y, vx, vy, r, invTH, invTS);
+                        D[k] = dv[u];
                     }
                 }
-                int cnt = 0;
+                inm = (uint32_t)quad_or((int)inm);
+                wsync();
 #pragma unroll
-                for (int k = 0; k < RMM; ++k) { cnt += inr[k] ? 1 : 0; L[k] = make_float4(0.f, 0.f, 0.f, 0.f); }
-#pragma unroll
-                for (int k = 0; k < RMM; ++k) {
-                    int rank = 0;
-#pragma unroll
-                    for (int q = 0; q < RMM; ++q)
-                        rank += (inr[q] && (d[q] < d[k] || (d[q] == d[k] && q < k))) ? 1 : 0;
-#pragma unroll
-                    for (int pp = 0; pp < RMM; ++pp)
-                        if (inr[k] && rank == pp) L[pp] = raw[k];
+                for (int u = 0; u < 3; ++u) {
+                    const int k = sq + 4 * u;
+                    if (k < M && ((inm >> k) & 1u)) {
+                        int rank = 0;
+                        for (int q = 0; q < M; ++q)
+                            if (((inm >> q) & 1u) && (D[q] < dv[u] || (D[q] == dv[u] && q < k))) ++rank;
+                        Lb[rank] = rawv[u];
+                    }
                 }
-#if defined(CN_ABL_NO_LP)
-                rx = L[0].x + L[8].y; ry = L[4].z + (float)cnt;   // timing-only ablation build
-#else
+                wsync();
+                const int cnt = __popc(inm);
+                const float vmq = sl.vmax[h];
+                float rx, ry;
                 STAMP_A(7);
-                const int fail_at = lp2_r(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
+                const int fail_at = lp2_q(Lb, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
                 STAMP_A(8);
-#if defined(CN_ABL_NO_LP3)
-                rx += (float)fail_at;                            // timing-only ablation build
-#else
-                if (fail_at < cnt) lp3_r(L, cnt, fail_at, my_vmax, rx, ry);
+                if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
                 STAMP_A(9);
-#endif
-#endif
-            } else {
-                float rq = rangeSq;
-                int cnt = 0;
-                const int maxN = M;
-                const int T = sl.T;
-                // KdTree: persisted agents_ order (identity at simulator creation)
-                uint8_t *perm = sl.perm;
-                for (int a = 0; a < A; ++a) perm[a * T + tid] = frozen ? S.o_perm[gh * A + a] : (uint8_t)a;
-                auto AX = [&](int a) -> float {
-                    if (a == 0) return X0;
-                    float x, y, vx, vy, r;
-                    slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
-                    return x;
-                };
-                auto AY = [&](int a) -> float {
-                    if (a == 0) return Y0;
-                    float x, y, vx, vy, r;
-                    slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
-                    return y;
-                };
-                // build (buildAgentTreeRecursive), iteratively; partitions perm in place
-                int stb[CN_MAX_A], ste[CN_MAX_A], sp = 0;
-                stb[sp] = 0; ste[sp] = A; ++sp;
-                while (sp > 0) {
-                    --sp;
-                    const int b = stb[sp], e = ste[sp];
-                    if (e - b <= 10) continue;
-                    float mnx = AX(perm[b * T + tid]), mxx = mnx;
-                    float mny = AY(perm[b * T + tid]), mxy = mny;
-                    for (int q = b + 1; q < e; ++q) {
-                        const int a = perm[q * T + tid];
-                        const float x = AX(a), y = AY(a);
-                        mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
-                        mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
-                    }
-                    const bool vert = (mxx - mnx > mxy - mny);
-                    const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
-                    int left = b, right = e;
-                    while (left < right) {
-                        while (left < right) {
-                            const int a = perm[left * T + tid];
-                            if (!((vert ? AX(a) : AY(a)) < split)) break;
-                            ++left;
-                        }
-                        while (right > left) {
-                            const int a = perm[(right - 1) * T + tid];
-                            if (!((vert ? AX(a) : AY(a)) >= split)) break;
-                            --right;
-                        }
-                        if (left < right) {
-                            const uint8_t t0 = perm[left * T + tid];
-                            perm[left * T + tid] = perm[(right - 1) * T + tid];
-                            perm[(right - 1) * T + tid] = t0;
-                            ++left; --right;
-                        }
-                    }
-                    if (left == b) { ++left; }
-                    stb[sp] = b; ste[sp] = left; ++sp;
-                    stb[sp] = left; ste[sp] = e; ++sp;
-                }
-                for (int a = 0; a < A; ++a) S.o_perm[gh * A + a] = perm[a * T + tid];
-                // query (queryAgentTreeRecursive): closer child first, ties -> right; subtree pruning
-                // never drops an in-range agent, so visiting every leaf inserts the same neighbours
-                sp = 0; stb[sp] = 0; ste[sp] = A; ++sp;
-                while (sp > 0) {
-                    --sp;
-                    const int b = stb[sp], e = ste[sp];
-                    if (e - b <= 10) {
-                        for (int q = b; q < e; ++q) {
-                            const int a = perm[q * T + tid];
-                            if (a == 0) continue;
-                            const float dx = X0 - AX(a), dy = Y0 - AY(a);
-                            insert_nbr(sl, tid, cnt, maxN, a - 1, dx * dx + dy * dy, rq);
-                        }
-                        continue;
-                    }
-                    float mnx = AX(perm[b * T + tid]), mxx = mnx;
-                    float mny = AY(perm[b * T + tid]), mxy = mny;
-                    for (int q = b + 1; q < e; ++q) {
-                        const int a = perm[q * T + tid];
-                        const float x = AX(a), y = AY(a);
-                        mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
-                        mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
-                    }
-                    const bool vert = (mxx - mnx > mxy - mny);
-                    const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
-                    int left = b;
-                    for (int q = b; q < e; ++q) {
-                        const int a = perm[q * T + tid];
-                        if ((vert ? AX(a) : AY(a)) < split) ++left;
-                    }
-                    if (left == b) ++left;
-                    float bb[2][4];
-                    for (int ch = 0; ch < 2; ++ch) {
-                        const int cb = ch ? left : b, ce = ch ? e : left;
-                        float a0x = AX(perm[cb * T + tid]), a1x = a0x;
-                        float a0y = AY(perm[cb * T + tid]), a1y = a0y;
-                        for (int q = cb + 1; q < ce; ++q) {
-                            const int a = perm[q * T + tid];
-                            const float x = AX(a), y = AY(a);
-                            a1x = a1x < x ? x : a1x; a0x = x < a0x ? x : a0x;
-                            a1y = a1y < y ? y : a1y; a0y = y < a0y ? y : a0y;
-                        }
-                        bb[ch][0] = a0x; bb[ch][1] = a1x; bb[ch][2] = a0y; bb[ch][3] = a1y;
-                    }
-                    const float dl = bbox_dist(X0, Y0, bb[0][0], bb[0][1], bb[0][2], bb[0][3]);
-                    const float dr = bbox_dist(X0, Y0, bb[1][0], bb[1][1], bb[1][2], bb[1][3]);
-                    if (dl < dr) {  // visit left first: push right, then left
-                        stb[sp] = left; ste[sp] = e; ++sp; stb[sp] = b; ste[sp] = left; ++sp;
-                    } else {
-                        stb[sp] = b; ste[sp] = left; ++sp; stb[sp] = left; ste[sp] = e; ++sp;
-                    }
-                }
-                // ORCA lines in neighbour order (Agent::computeNewVelocity, agents only)
-                LineView L{sl.lines, tid, T}, PL{sl.proj, tid, T};
-                for (int pq = 0; pq < cnt; ++pq) {
-                    const int k = sl.ns[pq * T + tid];
-                    float ox, oy, ovx, ovy, orr;
-                    slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, ox, oy, ovx, ovy, orr);
-                    L.set(pq, orca_line(X0, Y0, VX0, VY0, R0, ox, oy, ovx, ovy, orr, invTH, invTS));
-                }
-                const int fail_at = lp2(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
-                if (fail_at < cnt) lp3(L, PL, cnt, fail_at, my_vmax, rx, ry);
+                if (sq == 0) sl.nv[h] = make_double2((double)rx, (double)ry);
             }
-            nvx = (double)rx; nvy = (double)ry;
-        } else {
+        } else if (hl) {
+            const int eb = el * N;
+            const double px = HF(sl, H_PX, tid), py = HF(sl, H_PY, tid);
+            const double vx0 = HF(sl, H_VX, tid), vy0 = HF(sl, H_VY, tid);
+            const double rad = HF(sl, H_R, tid), vpref = HF(sl, H_VP, tid);
             // SOCIAL_FORCE.predict (social_force.py:11-66)
             const double dx = HF(sl, H_GX, tid) - px, dy = HF(sl, H_GY, tid) - py;
             const double dist = dsqrt(dx * dx + dy * dy);
@@ -1642,20 +1686,187 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
             const double n = np_norm2(nx, ny);
             if (n > vpref) { nvx = ddiv(nx, n) * vpref; nvy = ddiv(ny, n) * vpref; }
             else { nvx = nx; nvy = ny; }
+            sl.nv[tid] = make_double2(nvx, nvy);
         }
-        // per-human terms of calc_reward (crowd_sim.py:934-969), PRE-move
-        const double rdx = px - RF(sl, R_PX, el, EPB), rdy = py - RF(sl, R_PY, el, EPB);
-        sl.cd[tid] = dsqrt(rdx * rdx + rdy * rdy) - rad - RF(sl, R_RAD, el, EPB);
-#if defined(CN_ABL_NO_VR)
-        uint32_t f = 0u;
-#else
-        double hcx[4], hcy[4], rcx[4], rcy[4];
-        vel_rect(px, py, vx0, vy0, rad, false, hcx, hcy);
-        for (int k = 0; k < 4; ++k) { rcx[k] = sl.rvr[k * EPB + el]; rcy[k] = sl.rvr[(4 + k) * EPB + el]; }
-        uint32_t f = quads_intersect(rcx, rcy, hcx, hcy) ? LF_VR : 0u;
-#endif
-        if (!(np_norm2(px - HF(sl, H_GX, tid), py - HF(sl, H_GY, tid)) < rad)) f |= LF_NOTREACHED;
-        sl.lf[tid] = f;
+        // per-human reward terms on wave 1's lanes, beside their ORCA share
+        if (tid >= 64 && tid - 64 < nh) reward_terms(tid - 64);
+        __syncthreads();
+        if (hl) { nvx = sl.nv[tid].x; nvy = sl.nv[tid].y; }
+    } else {
+        if (hl) {
+            const int eb = el * N;
+            const double px = HF(sl, H_PX, tid), py = HF(sl, H_PY, tid);
+            const double vx0 = HF(sl, H_VX, tid), vy0 = HF(sl, H_VY, tid);
+            const double rad = HF(sl, H_R, tid), vpref = HF(sl, H_VP, tid);
+            if (orca) {
+                const float rdummy = (float)(c.human_radius + 0.01 + c.orca_safety_space);
+                const float X0 = (float)px, Y0 = (float)py, VX0 = (float)vx0, VY0 = (float)vy0;
+                const float R0 = sl.orad[tid];
+                const float rangeSq = (float)c.orca_neighbor_dist * (float)c.orca_neighbor_dist;
+                const float invTH = fdiv(1.0f, (float)c.orca_time_horizon);
+                const float invTS = fdiv(1.0f, (float)dt);
+                // preferred velocity: unit vector to the goal only if farther than 1 (orca.py:118-122)
+                double gdx = HF(sl, H_GX, tid) - px, gdy = HF(sl, H_GY, tid) - py;
+                const double speed = np_norm2(gdx, gdy);
+                if (speed > 1.0) { gdx = ddiv(gdx, speed); gdy = ddiv(gdy, speed); }
+                float rx, ry;
+                {
+                    float rq = rangeSq;
+                    int cnt = 0;
+                    const int maxN = M;
+                    const int T = sl.T;
+                    // KdTree: persisted agents_ order (identity at simulator creation)
+                    uint8_t *perm = sl.perm;
+                    for (int a = 0; a < A; ++a) perm[a * T + tid] = frozen ? S.o_perm[gh * A + a] : (uint8_t)a;
+                    auto AX = [&](int a) -> float {
+                        if (a == 0) return X0;
+                        float x, y, vx, vy, r;
+                        slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
+                        return x;
+                    };
+                    auto AY = [&](int a) -> float {
+                        if (a == 0) return Y0;
+                        float x, y, vx, vy, r;
+                        slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
+                        return y;
+                    };
+                    // build (buildAgentTreeRecursive), iteratively; partitions perm in place
+                    int stb[CN_MAX_A], ste[CN_MAX_A], sp = 0;
+                    stb[sp] = 0; ste[sp] = A; ++sp;
+                    while (sp > 0) {
+                        --sp;
+                        const int b = stb[sp], e = ste[sp];
+                        if (e - b <= 10) continue;
+                        float mnx = AX(perm[b * T + tid]), mxx = mnx;
+                        float mny = AY(perm[b * T + tid]), mxy = mny;
+                        for (int q = b + 1; q < e; ++q) {
+                            const int a = perm[q * T + tid];
+                            const float x = AX(a), y = AY(a);
+                            mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
+                            mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
+                        }
+                        const bool vert = (mxx - mnx > mxy - mny);
+                        const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
+                        int left = b, right = e;
+                        while (left < right) {
+                            while (left < right) {
+                                const int a = perm[left * T + tid];
+                                if (!((vert ? AX(a) : AY(a)) < split)) break;
+                                ++left;
+                            }
+                            while (right > left) {
+                                const int a = perm[(right - 1) * T + tid];
+                                if (!((vert ? AX(a) : AY(a)) >= split)) break;
+                                --right;
+                            }
+                            if (left < right) {
+                                const uint8_t t0 = perm[left * T + tid];
+                                perm[left * T + tid] = perm[(right - 1) * T + tid];
+                                perm[(right - 1) * T + tid] = t0;
+                                ++left; --right;
+                            }
+                        }
+                        if (left == b) { ++left; }
+                        stb[sp] = b; ste[sp] = left; ++sp;
+                        stb[sp] = left; ste[sp] = e; ++sp;
+                    }
+                    for (int a = 0; a < A; ++a) S.o_perm[gh * A + a] = perm[a * T + tid];
+                    // query (queryAgentTreeRecursive): closer child first, ties -> right; subtree pruning
+                    // never drops an in-range agent, so visiting every leaf inserts the same neighbours
+                    sp = 0; stb[sp] = 0; ste[sp] = A; ++sp;
+                    while (sp > 0) {
+                        --sp;
+                        const int b = stb[sp], e = ste[sp];
+                        if (e - b <= 10) {
+                            for (int q = b; q < e; ++q) {
+                                const int a = perm[q * T + tid];
+                                if (a == 0) continue;
+                                const float dx = X0 - AX(a), dy = Y0 - AY(a);
+                                insert_nbr(sl, tid, cnt, maxN, a - 1, dx * dx + dy * dy, rq);
+                            }
+                            continue;
+                        }
+                        float mnx = AX(perm[b * T + tid]), mxx = mnx;
+                        float mny = AY(perm[b * T + tid]), mxy = mny;
+                        for (int q = b + 1; q < e; ++q) {
+                            const int a = perm[q * T + tid];
+                            const float x = AX(a), y = AY(a);
+                            mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
+                            mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
+                        }
+                        const bool vert = (mxx - mnx > mxy - mny);
+                        const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
+                        int left = b;
+                        for (int q = b; q < e; ++q) {
+                            const int a = perm[q * T + tid];
+                            if ((vert ? AX(a) : AY(a)) < split) ++left;
+                        }
+                        if (left == b) ++left;
+                        float bb[2][4];
+                        for (int ch = 0; ch < 2; ++ch) {
+                            const int cb = ch ? left : b, ce = ch ? e : left;
+                            float a0x = AX(perm[cb * T + tid]), a1x = a0x;
+                            float a0y = AY(perm[cb * T + tid]), a1y = a0y;
+                            for (int q = cb + 1; q < ce; ++q) {
+                                const int a = perm[q * T + tid];
+                                const float x = AX(a), y = AY(a);
+                                a1x = a1x < x ? x : a1x; a0x = x < a0x ? x : a0x;
+                                a1y = a1y < y ? y : a1y; a0y = y < a0y ? y : a0y;
+                            }
+                            bb[ch][0] = a0x; bb[ch][1] = a1x; bb[ch][2] = a0y; bb[ch][3] = a1y;
+                        }
+                        const float dl = bbox_dist(X0, Y0, bb[0][0], bb[0][1], bb[0][2], bb[0][3]);
+                        const float dr = bbox_dist(X0, Y0, bb[1][0], bb[1][1], bb[1][2], bb[1][3]);
+                        if (dl < dr) {  // visit left first: push right, then left
+                            stb[sp] = left; ste[sp] = e; ++sp; stb[sp] = b; ste[sp] = left; ++sp;
+                        } else {
+                            stb[sp] = b; ste[sp] = left; ++sp; stb[sp] = left; ste[sp] = e; ++sp;
+                        }
+                    }
+                    // ORCA lines in neighbour order (Agent::computeNewVelocity, agents only)
+                    LineView L{sl.lines, tid, T}, PL{sl.proj, tid, T};
+                    for (int pq = 0; pq < cnt; ++pq) {
+                        const int k = sl.ns[pq * T + tid];
+                        float ox, oy, ovx, ovy, orr;
+                        slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, ox, oy, ovx, ovy, orr);
+                        L.set(pq, orca_line(X0, Y0, VX0, VY0, R0, ox, oy, ovx, ovy, orr, invTH, invTS));
+                    }
+                    const int fail_at = lp2(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
+                    if (fail_at < cnt) lp3(L, PL, cnt, fail_at, my_vmax, rx, ry);
+                }
+                nvx = (double)rx; nvy = (double)ry;
+            } else {
+                // SOCIAL_FORCE.predict (social_force.py:11-66)
+                const double dx = HF(sl, H_GX, tid) - px, dy = HF(sl, H_GY, tid) - py;
+                const double dist = dsqrt(dx * dx + dy * dy);
+                const double dvx = ddiv(dx, dist) * vpref, dvy = ddiv(dy, dist) * vpref;
+                const double cdx = c.sf_KI * (dvx - vx0), cdy = c.sf_KI * (dvy - vy0);
+                double ix = 0.0, iy = 0.0;
+                for (int k = 0; k < M; ++k) {
+                    double ox, oy, orr;
+                    const bool v = (vis >> k) & 1u;
+                    if (k < N - 1) {
+                        const int j = eb + (k < i ? k : k + 1);
+                        ox = v ? HF(sl, H_PX, j) : CN_DUMMY_POS; oy = v ? HF(sl, H_PY, j) : CN_DUMMY_POS;
+                        orr = v ? HF(sl, H_R, j) : c.human_radius;
+                    } else {
+                        ox = v ? RF(sl, R_PX, el, EPB) : CN_DUMMY_POS; oy = v ? RF(sl, R_PY, el, EPB) : CN_DUMMY_POS;
+                        orr = v ? RF(sl, R_RAD, el, EPB) : c.robot_radius;
+                    }
+                    const double ddx = px - ox, ddy = py - oy;
+                    const double d = dsqrt(ddx * ddx + ddy * ddy);
+                    const double ex = exp(ddiv(rad + orr - d, c.sf_B));
+                    ix += c.sf_A * ex * ddiv(ddx, d);
+                    iy += c.sf_A * ex * ddiv(ddy, d);
+                }
+                const double tx = (cdx + ix) * dt, ty = (cdy + iy) * dt;
+                const double nx = vx0 + tx, ny = vy0 + ty;
+                const double n = np_norm2(nx, ny);
+                if (n > vpref) { nvx = ddiv(nx, n) * vpref; nvy = ddiv(ny, n) * vpref; }
+                else { nvx = nx; nvy = ny; }
+            }
+            reward_terms(tid);
+        }
     }
     __syncthreads();
     STAMP_A(3);
@@ -1862,8 +2073,8 @@ __global__ void __launch_bounds__(CN_BLK) cn_step_kernel(StepArgs g, cn_config c
     // earlier launch; an env reset by the previous launch (ep_len == 1) may be redrawn by this launch's
     // spawn waves right now, so it (and every env after cn_reset/cn_set_state) draws inline instead.
     {
-        const int nw = sl.T / 64, w = tid / 64, lane = tid & 63;
-        char *wb = smem + P.o_lines + w * CN_PEND_LDS;   // over the ORCA scratch, dead after phase 2
+        const int nw = P.rng_waves, w = tid / 64, lane = tid & 63;
+        char *wb = smem + P.o_lines + (w < nw ? w : 0) * CN_PEND_LDS;   // over the ORCA scratch, dead after phase 2
         WRng m;
         m.w = (uint32_t *)wb; m.lane = lane;
         m.sl = (double *)(wb + 2 * CN_MT_N * 4 + 7 * 32 * 8);
@@ -1990,6 +2201,7 @@ struct cn_engine {
     PendPtrs pend;
     int pend_all;         // next kernel A draws every env's spawn (after cn_reset / cn_set_state)
     int pend_blocks;      // spare workgroups of kernel A running spawn waves
+    int pend_waves;       // spawning waves per spare workgroup
     int a_lds;            // kernel A dynamic LDS: max(step plan, spawn waves)
     int64_t case_size, counter_offset;
     int rng_grid;
@@ -2121,13 +2333,15 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     }
     g->pend_all = 1;
     {
-        const int nw = g->plan.T / 64;
+        // the plan holds phase 5's RNG regions (laid over the ORCA scratch); spare workgroups run as many
+        // spawning waves as regions fit in the same allocation
+        g->a_lds = g->plan.total;
+        const int fit = g->a_lds / CN_PEND_LDS;
+        g->pend_waves = fit < g->plan.T / 64 ? fit : g->plan.T / 64;
+        const int nw = g->pend_waves;
         const int64_t need = (E + nw - 1) / nw;
-        const int cap = 256 / nw;
+        const int cap = 128 / nw;   // ~128 spawning waves; leaves the step workgroups co-resident
         g->pend_blocks = (int)(need < cap ? need : cap);
-        // one RNG region per wave for phase 5, laid over the ORCA scratch (lines, projections, kd order)
-        const int lds_need = g->plan.o_lines + nw * CN_PEND_LDS;
-        g->a_lds = g->plan.total > lds_need ? g->plan.total : lds_need;
     }
     cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
     // unit-circle table of GEOS's 64-gon point buffer (norm zones)
@@ -2237,6 +2451,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.pend.P = g->pend; a.pend.list = g->plist + (int64_t)kr * (g->E + 64); a.pend.count = g->work_count + 2 + kr;
     a.pend.all = g->pend_all;
     a.pend.step_blocks = blocks; a.pend.pend_blocks = g->pend_blocks; a.pend.counter_offset = g->counter_offset;
+    a.pend.waves = g->pend_waves;
     g->pend_all = 0;
     const int grid = blocks + g->pend_blocks;
     if (g->plan.kd)
