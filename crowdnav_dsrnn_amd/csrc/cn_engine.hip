@@ -39,7 +39,7 @@ __device__ __forceinline__ void wsync()
 // Diagnostic build only (-DCN_STAMPS): per-workgroup s_memtime stamps at phase boundaries, read back
 // with cn_debug_stamps(). The shipped library is built without it (no stamp executes).
 #ifdef CN_STAMPS
-#define CN_NSTAMP 12
+#define CN_NSTAMP 16
 __device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 #define STAMP_A(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + (k)] = clock64(); } while (0)
@@ -67,8 +67,8 @@ struct StepPlan {
     int rng_waves;   // phase-5 RNG regions (CN_PEND_LDS each), laid over o_lines
 };
 
-#define CN_RENV_F 14   // robot/env doubles per env in LDS
-#define CN_HUM_F 9     // human doubles per lane in LDS
+#define CN_RENV_F 17   // robot/env doubles per env in LDS
+#define CN_HUM_F 14    // human doubles per lane in LDS
 #define CN_PEND_LDS (2 * CN_MT_N * 4 + 7 * 32 * 8 + 6 * 64 * 8)   // per RNG wave: MT ring, agent table, try slots
 
 __host__ __device__ inline int cn_align16(int x) { return (x + 15) & ~15; }
@@ -129,8 +129,8 @@ struct SL {
     uint8_t *ns;      // [M][T]
     uint8_t *perm;    // [A][T]
 };
-enum { R_PX, R_PY, R_GX, R_GY, R_VX, R_VY, R_TH, R_RAD, R_VP, R_POT, R_GT, R_DV, R_NX, R_NY };
-enum { H_PX, H_PY, H_GX, H_GY, H_VX, H_VY, H_R, H_VP, H_TH };
+enum { R_PX, R_PY, R_GX, R_GY, R_VX, R_VY, R_TH, R_RAD, R_VP, R_POT, R_GT, R_DV, R_NX, R_NY, R_LAX, R_LAY, R_EPR };
+enum { H_PX, H_PY, H_GX, H_GY, H_VX, H_VY, H_R, H_VP, H_TH, H_BPX, H_BPY, H_BVX, H_BVY, H_BR };
 #define RF(sl, f, el, EPB) ((sl).r[(f) * (EPB) + (el)])
 #define HF(sl, f, t) ((sl).h[(f) * (sl).T + (t)])
 
@@ -1459,18 +1459,20 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     const int el = tid / N, i = tid - el * N;
     const bool hl = el < nenv_here;               // human lane
     const int64_t gh = (int64_t)(e0 + el) * N + i;  // global human index
-    const bool rl = tid < nenv_here;              // env lane (robot / reward / bookkeeping)
-    const int64_t ge = e0 + tid;
+    // env lanes (robot / reward / bookkeeping): wave 1 on the quad path, so they run beside the human
+    // lanes of wave 0 in phases 0, 3 and 4; the first lanes on the kd-tree path
+    const int re = KD ? tid : tid - 64;
+    const bool rl = re >= 0 && re < nenv_here;
+    const int64_t ge = e0 + re;
     const bool holo = c.kinematics == CN_HOLONOMIC;
     const double dt = c.time_step;
 
     STAMP_A(0);
     // ---- phase 0: load state into LDS -----------------------------------------------------------
-    double bpx = 0, bpy = 0, bvx = 0, bvy = 0, br = 0;
-    // values needed in later phases are loaded here, so their latency overlaps phase 0
+    // values needed in later phases are loaded here, so their latency overlaps phase 0 (doubles parked
+    // in LDS rather than registers across the ORCA phase)
     float pre_or = 0.0f, pre_vmax = 0.0f;
     uint32_t pre_dm = 0u;
-    double pre_lax = 0, pre_lay = 0, pre_epr = 0;
     int32_t pre_epl = 0, pre_sc = 0;
     uint32_t pre_ovf = 0;
     if (hl) {
@@ -1480,40 +1482,46 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         HF(sl, H_VX, tid) = S.h_vx[gh]; HF(sl, H_VY, tid) = S.h_vy[gh];
         HF(sl, H_R, tid) = S.h_r[gh]; HF(sl, H_VP, tid) = S.h_vpref[gh];
         HF(sl, H_TH, tid) = S.h_theta[gh];
-        bpx = S.b_px[gh]; bpy = S.b_py[gh]; bvx = S.b_vx[gh]; bvy = S.b_vy[gh]; br = S.b_r[gh];
+        HF(sl, H_BPX, tid) = S.b_px[gh]; HF(sl, H_BPY, tid) = S.b_py[gh]; HF(sl, H_BVX, tid) = S.b_vx[gh];
+        HF(sl, H_BVY, tid) = S.b_vy[gh]; HF(sl, H_BR, tid) = S.b_r[gh];
     }
+    STAMP_A(12);
     if (rl) {
-        RF(sl, R_PX, tid, EPB) = S.r_px[ge]; RF(sl, R_PY, tid, EPB) = S.r_py[ge];
-        RF(sl, R_GX, tid, EPB) = S.r_gx[ge]; RF(sl, R_GY, tid, EPB) = S.r_gy[ge];
-        RF(sl, R_VX, tid, EPB) = S.r_vx[ge]; RF(sl, R_VY, tid, EPB) = S.r_vy[ge];
-        RF(sl, R_TH, tid, EPB) = S.r_theta[ge]; RF(sl, R_RAD, tid, EPB) = S.r_radius[ge];
-        RF(sl, R_VP, tid, EPB) = S.r_vpref[ge]; RF(sl, R_POT, tid, EPB) = S.potential[ge];
-        RF(sl, R_GT, tid, EPB) = S.gtime[ge]; RF(sl, R_DV, tid, EPB) = S.r_dv[ge];
-        sl.rflag[tid] = S.flags[ge];
-        pre_lax = S.last_ax[ge]; pre_lay = S.last_ay[ge]; pre_epr = S.ep_return[ge]; pre_epl = S.ep_len[ge];
+        RF(sl, R_PX, re, EPB) = S.r_px[ge]; RF(sl, R_PY, re, EPB) = S.r_py[ge];
+        RF(sl, R_GX, re, EPB) = S.r_gx[ge]; RF(sl, R_GY, re, EPB) = S.r_gy[ge];
+        RF(sl, R_VX, re, EPB) = S.r_vx[ge]; RF(sl, R_VY, re, EPB) = S.r_vy[ge];
+        RF(sl, R_TH, re, EPB) = S.r_theta[ge]; RF(sl, R_RAD, re, EPB) = S.r_radius[ge];
+        RF(sl, R_VP, re, EPB) = S.r_vpref[ge]; RF(sl, R_POT, re, EPB) = S.potential[ge];
+        RF(sl, R_GT, re, EPB) = S.gtime[ge]; RF(sl, R_DV, re, EPB) = S.r_dv[ge];
+        sl.rflag[re] = S.flags[ge];
+        RF(sl, R_LAX, re, EPB) = S.last_ax[ge]; RF(sl, R_LAY, re, EPB) = S.last_ay[ge];
+        RF(sl, R_EPR, re, EPB) = S.ep_return[ge]; pre_epl = S.ep_len[ge];
         pre_sc = S.scenario[ge]; pre_ovf = S.overflow[ge];
+        STAMP_A(13);
         // ---- SRNN.clip_action (srnn.py:18-48) + unicycle integrator (crowd_sim_dict.py:211-217)
         float a0 = g.actions[ge * 2], a1 = g.actions[ge * 2 + 1];
         if (holo) {
             const float n = np_norm2f(a0, a1);
-            if ((double)n > RF(sl, R_VP, tid, EPB)) {
-                const float vp = (float)RF(sl, R_VP, tid, EPB);
+            if ((double)n > RF(sl, R_VP, re, EPB)) {
+                const float vp = (float)RF(sl, R_VP, re, EPB);
                 a0 = fdiv(a0, n) * vp; a1 = fdiv(a1, n) * vp;
             }
         } else {
             a0 = np_clipf(a0, -0.1f, 0.1f);
             a1 = np_clipf(a1, -0.1f, 0.1f);
-            const float vp = (float)RF(sl, R_VP, tid, EPB);
-            const float dv = np_clipf((float)RF(sl, R_DV, tid, EPB) + a0, -vp, vp);
-            RF(sl, R_DV, tid, EPB) = dv;
+            const float vp = (float)RF(sl, R_VP, re, EPB);
+            const float dv = np_clipf((float)RF(sl, R_DV, re, EPB) + a0, -vp, vp);
+            RF(sl, R_DV, re, EPB) = dv;
             a0 = dv;
         }
-        sl.act[tid] = a0; sl.act[EPB + tid] = a1;
+        sl.act[re] = a0; sl.act[EPB + re] = a1;
+        STAMP_A(10);
         // robot VelocityRectangle (pre-move)
         double cx[4], cy[4];
-        vel_rect(RF(sl, R_PX, tid, EPB), RF(sl, R_PY, tid, EPB), RF(sl, R_VX, tid, EPB), RF(sl, R_VY, tid, EPB),
-                 RF(sl, R_RAD, tid, EPB), (sl.rflag[tid] & CN_FLAG_ROBOT_F32) != 0, cx, cy);
-        for (int k = 0; k < 4; ++k) { sl.rvr[k * EPB + tid] = cx[k]; sl.rvr[(4 + k) * EPB + tid] = cy[k]; }
+        vel_rect(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB), RF(sl, R_VY, re, EPB),
+                 RF(sl, R_RAD, re, EPB), (sl.rflag[re] & CN_FLAG_ROBOT_F32) != 0, cx, cy);
+        for (int k = 0; k < 4; ++k) { sl.rvr[k * EPB + re] = cx[k]; sl.rvr[(4 + k) * EPB + re] = cy[k]; }
+        STAMP_A(11);
     }
     __syncthreads();
     STAMP_A(1);
@@ -1873,12 +1881,12 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
 
     // ---- phase 3: calc_reward ladder + robot kinematics + Monitor (env lanes) ---------------------
     if (rl) {
-        const double rpx = RF(sl, R_PX, tid, EPB), rpy = RF(sl, R_PY, tid, EPB), rr = RF(sl, R_RAD, tid, EPB);
-        const double rgx = RF(sl, R_GX, tid, EPB), rgy = RF(sl, R_GY, tid, EPB);
-        const uint32_t flags = sl.rflag[tid];
+        const double rpx = RF(sl, R_PX, re, EPB), rpy = RF(sl, R_PY, re, EPB), rr = RF(sl, R_RAD, re, EPB);
+        const double rgx = RF(sl, R_GX, re, EPB), rgy = RF(sl, R_GY, re, EPB);
+        const uint32_t flags = sl.rflag[re];
         const bool rf32 = (flags & CN_FLAG_ROBOT_F32) != 0;
-        const float a0 = sl.act[tid], a1 = sl.act[EPB + tid];
-        const int eb = tid * N;
+        const float a0 = sl.act[re], a1 = sl.act[EPB + re];
+        const int eb = re * N;
         double dmin = INFINITY;
         bool collision = false, nz_viol = false, nz_checked = false;
         int vr_viol = 0, agg = 0;
@@ -1890,7 +1898,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 nz_checked = true;
                 double zx[4], zy[4];
                 for (int z = 0; z < 2 && !nz_viol; ++z) {
-                    norm_zone(rpx, rpy, RF(sl, R_VX, tid, EPB), RF(sl, R_VY, tid, EPB), rr, rf32, c.norm_zone_lhs,
+                    norm_zone(rpx, rpy, RF(sl, R_VX, re, EPB), RF(sl, R_VY, re, EPB), rr, rf32, c.norm_zone_lhs,
                               z == 0, zx, zy);
                     if (disc_quad_intersect(rpx, rpy, rr, zx, zy)) nz_viol = true;
                 }
@@ -1902,7 +1910,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const bool reaching_goal = np_norm2(rpx - rgx, rpy - rgy) < rr;
         if (!reaching_goal) ++agg;
         // commanded world-frame velocity; unicycle: theta + r is float32 (NEP 50)
-        const float tr = (float)RF(sl, R_TH, tid, EPB) + a1;
+        const float tr = (float)RF(sl, R_TH, re, EPB) + a1;
         const float th_new = np_modf(tr, (float)(2 * CN_PI));
         double cvx, cvy;
         if (holo) { cvx = a0; cvy = a1; }
@@ -1912,7 +1920,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         if (!holo && !(fabsf(a1) < 0.0001f)) {
             const float w = fdiv(a1, (float)dt);
             const float R = fdiv(a0, w);
-            const double th = RF(sl, R_TH, tid, EPB);
+            const double th = RF(sl, R_TH, re, EPB);
             double t1x, t1y;
             if (rf32) { t1x = (double)(R * np_sinf((float)th)); t1y = (double)(R * np_cosf((float)th)); }
             else { t1x = (double)R * sin(th); t1y = (double)R * cos(th); }
@@ -1930,8 +1938,8 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         }
         double jerk;
         {
-            const float ax = (float)cvx - (float)RF(sl, R_VX, tid, EPB), ay = (float)cvy - (float)RF(sl, R_VY, tid, EPB);
-            const float dax = ax - (float)pre_lax, day = ay - (float)pre_lay;
+            const float ax = (float)cvx - (float)RF(sl, R_VX, re, EPB), ay = (float)cvy - (float)RF(sl, R_VY, re, EPB);
+            const float dax = ax - (float)RF(sl, R_LAX, re, EPB), day = ay - (float)RF(sl, R_LAY, re, EPB);
             jerk = (double)(dax * dax + day * day);
             S.last_ax[ge] = ax; S.last_ay[ge] = ay;
         }
@@ -1939,7 +1947,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const bool inside = inside_world(rpx, rpy, rr, c.square_width / 2);
         double speed;
         { const float fx = (float)cvx, fy = (float)cvy; speed = (double)fsqrt(fx * fx + fy * fy); }
-        const double gt = RF(sl, R_GT, tid, EPB);
+        const double gt = RF(sl, R_GT, re, EPB);
         double reward;
         int done, event;
         if (gt >= c.time_limit - 1) { reward = 0; done = 1; event = CN_EV_TIMEOUT; }
@@ -1952,8 +1960,8 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             reward = (dmin - c.discomfort_dist) * c.discomfort_penalty_factor;
             done = 0; event = CN_EV_DANGER;
         } else {
-            reward = c.potential_factor * (-fabs(dist_to_goal) - RF(sl, R_POT, tid, EPB));
-            RF(sl, R_POT, tid, EPB) = -fabs(dist_to_goal);
+            reward = c.potential_factor * (-fabs(dist_to_goal) - RF(sl, R_POT, re, EPB));
+            RF(sl, R_POT, re, EPB) = -fabs(dist_to_goal);
             if (c.norm_zones && nz_viol) reward += c.norm_zone_penalty;
             done = 0; event = CN_EV_NOTHING;
         }
@@ -1980,17 +1988,17 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         }
         // robot kinematics (agent.py:198-212)
         if (holo) {
-            RF(sl, R_NX, tid, EPB) = rpx + (double)(a0 * (float)dt);
-            RF(sl, R_NY, tid, EPB) = rpy + (double)(a1 * (float)dt);
-            RF(sl, R_VX, tid, EPB) = a0; RF(sl, R_VY, tid, EPB) = a1;
+            RF(sl, R_NX, re, EPB) = rpx + (double)(a0 * (float)dt);
+            RF(sl, R_NY, re, EPB) = rpy + (double)(a1 * (float)dt);
+            RF(sl, R_VX, re, EPB) = a0; RF(sl, R_VY, re, EPB) = a1;
         } else {
-            RF(sl, R_NX, tid, EPB) = upx; RF(sl, R_NY, tid, EPB) = upy;
-            RF(sl, R_TH, tid, EPB) = th_new;
-            RF(sl, R_VX, tid, EPB) = cvx; RF(sl, R_VY, tid, EPB) = cvy;
+            RF(sl, R_NX, re, EPB) = upx; RF(sl, R_NY, re, EPB) = upy;
+            RF(sl, R_TH, re, EPB) = th_new;
+            RF(sl, R_VX, re, EPB) = cvx; RF(sl, R_VY, re, EPB) = cvy;
         }
-        sl.rflag[tid] = flags | CN_FLAG_ROBOT_F32;
-        RF(sl, R_GT, tid, EPB) = gt + dt;
-        const double epr = pre_epr + reward;
+        sl.rflag[re] = flags | CN_FLAG_ROBOT_F32;
+        RF(sl, R_GT, re, EPB) = gt + dt;
+        const double epr = RF(sl, R_EPR, re, EPB) + reward;
         const int32_t epl = pre_epl + 1;
         S.ep_return[ge] = epr; S.ep_len[ge] = epl;
         if (g.reward) g.reward[ge] = (float)reward;
@@ -1998,7 +2006,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         if (g.event) g.event[ge] = (int8_t)event;
         if (g.ep_return) g.ep_return[ge] = epr;
         if (g.ep_len) g.ep_len[ge] = epl;
-        sl.rflag[EPB + tid] = (uint32_t)done;   // aux word: done
+        sl.rflag[EPB + re] = (uint32_t)done;   // aux word: done
     }
     __syncthreads();
     STAMP_A(4);
@@ -2018,10 +2026,12 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             else fov_dir32((float)RF(sl, R_TH, el, EPB), fx, fy);
             rv = in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov) ? 1 : 0;
         }
+        double bpx, bpy, bvx, bvy, br;
         if (rv) {
             bpx = npx; bpy = npy; bvx = nvx; bvy = nvy; br = HF(sl, H_R, tid);
         } else {
-            bpx = bpx + bvx * dt; bpy = bpy + bvy * dt;
+            bvx = HF(sl, H_BVX, tid); bvy = HF(sl, H_BVY, tid); br = HF(sl, H_BR, tid);
+            bpx = HF(sl, H_BPX, tid) + bvx * dt; bpy = HF(sl, H_BPY, tid) + bvy * dt;
         }
         S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = bvx; S.b_vy[gh] = bvy; S.b_r[gh] = br;
         g.spatial[gh * 2] = (float)(bpx - rnx);
@@ -2034,35 +2044,35 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     }
     __syncthreads();
     if (rl) {
-        const double nx = RF(sl, R_NX, tid, EPB), ny = RF(sl, R_NY, tid, EPB);
+        const double nx = RF(sl, R_NX, re, EPB), ny = RF(sl, R_NY, re, EPB);
         S.r_px[ge] = nx; S.r_py[ge] = ny;
-        S.r_vx[ge] = RF(sl, R_VX, tid, EPB); S.r_vy[ge] = RF(sl, R_VY, tid, EPB);
-        S.r_theta[ge] = RF(sl, R_TH, tid, EPB);
-        S.r_dv[ge] = RF(sl, R_DV, tid, EPB);
-        S.potential[ge] = RF(sl, R_POT, tid, EPB);
-        const double gt = RF(sl, R_GT, tid, EPB);
+        S.r_vx[ge] = RF(sl, R_VX, re, EPB); S.r_vy[ge] = RF(sl, R_VY, re, EPB);
+        S.r_theta[ge] = RF(sl, R_TH, re, EPB);
+        S.r_dv[ge] = RF(sl, R_DV, re, EPB);
+        S.potential[ge] = RF(sl, R_POT, re, EPB);
+        const double gt = RF(sl, R_GT, re, EPB);
         S.gtime[ge] = gt;
-        uint32_t flags = sl.rflag[tid];
+        uint32_t flags = sl.rflag[re];
         if (orca) flags |= CN_FLAG_ORCA_FROZEN;
         bool endg = false, nan = false;
         for (int k = 0; k < N; ++k) {
-            const uint32_t f = sl.lf[tid * N + k];
+            const uint32_t f = sl.lf[re * N + k];
             endg |= (f & LF_ENDGOAL) != 0;
             nan |= (f & 0x80000000u) != 0;
         }
         if (nan) flags |= CN_FLAG_NAN;
         S.flags[ge] = flags;
         float *rn = g.robot_node + ge * 7;
-        rn[0] = (float)nx; rn[1] = (float)ny; rn[2] = (float)RF(sl, R_RAD, tid, EPB);
-        rn[3] = (float)RF(sl, R_GX, tid, EPB); rn[4] = (float)RF(sl, R_GY, tid, EPB);
-        rn[5] = (float)RF(sl, R_VP, tid, EPB); rn[6] = (float)RF(sl, R_TH, tid, EPB);
-        g.temporal[ge * 2] = (float)RF(sl, R_VX, tid, EPB);
-        g.temporal[ge * 2 + 1] = (float)RF(sl, R_VY, tid, EPB);
+        rn[0] = (float)nx; rn[1] = (float)ny; rn[2] = (float)RF(sl, R_RAD, re, EPB);
+        rn[3] = (float)RF(sl, R_GX, re, EPB); rn[4] = (float)RF(sl, R_GY, re, EPB);
+        rn[5] = (float)RF(sl, R_VP, re, EPB); rn[6] = (float)RF(sl, R_TH, re, EPB);
+        g.temporal[ge * 2] = (float)RF(sl, R_VX, re, EPB);
+        g.temporal[ge * 2 + 1] = (float)RF(sl, R_VY, re, EPB);
         // random numbers needed? (crowd_sim_dict.py:260-269, shmem_vec_env.py:166-167)
-        const bool done = sl.rflag[EPB + tid] != 0;
+        const bool done = sl.rflag[EPB + re] != 0;
         const bool rgoal = c.random_goal_changing && np_mod(gt, 5.0) == 0.0;
         const bool egoal = c.end_goal_changing && endg;
-        sl.rflag[EPB + tid] = (done ? 1u : 0u) | (rgoal ? 2u : 0u) | (egoal ? 4u : 0u) |
+        sl.rflag[EPB + re] = (done ? 1u : 0u) | (rgoal ? 2u : 0u) | (egoal ? 4u : 0u) |
                               (pre_epl + 1 == 1 ? 8u : 0u);
     }
     __syncthreads();

@@ -29,8 +29,8 @@ def run(variant, E=4096, N=10, steps=300):
     eng.reset()
     L = _lib.lib()
     L.cn_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    a = np.zeros(4096 * 12, np.uint64)
-    b = np.zeros(8192 * 12, np.uint64)
+    a = np.zeros(4096 * 16, np.uint64)
+    b = np.zeros(8192 * 16, np.uint64)
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
     acts = torch.rand((steps, E, 2), generator=g, device="cuda:0") * 0.2 - 0.1
@@ -43,7 +43,7 @@ def run(variant, E=4096, N=10, steps=300):
     L.cn_debug_stamps(a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p))
     T = 64 if N <= 10 else (256 if N <= 12 else 128)
     blocks = (E + (T // N) - 1) // (T // N)
-    A = a.reshape(-1, 12)[:blocks].astype(np.int64)
+    A = a.reshape(-1, 16)[:blocks].astype(np.int64)
     d = np.diff(A[:, :7], axis=1)
     print("[%s] kernel A avg %.1f us, kernel B avg %.1f us over %d steps" % (variant, ta.value * 1e3 / n.value,
                                                                           tb.value * 1e3 / n.value, n.value))
@@ -53,9 +53,10 @@ def run(variant, E=4096, N=10, steps=300):
     for k, nm in enumerate(names):
         print("    %-26s median %8d  max %8d  (%.0f%%)" % (nm, np.median(d[:, k]), d[:, k].max(),
                                                             100 * np.median(d[:, k]) / np.median(tot)))
-    B = b.reshape(-1, 12).astype(np.int64)[:E]
+    B = b.reshape(-1, 16).astype(np.int64)[:E]
     t0 = A[:, 0].min()
-    sub = [("lines+sort", A[:, 7] - A[:, 2]), ("LP2", A[:, 8] - A[:, 7]), ("LP3", A[:, 9] - A[:, 8]), ("VR+terms", A[:, 3] - A[:, 9])]
+    sub = [("p0 human loads", A[:, 12] - A[:, 0]), ("p0 env loads", A[:, 13] - A[:, 12]), ("p0 clip", A[:, 10] - A[:, 13]), ("p0 robot VR", A[:, 11] - A[:, 10]), ("p0 barrier", A[:, 1] - A[:, 11]),
+           ("lines+sort", A[:, 7] - A[:, 2]), ("LP2", A[:, 8] - A[:, 7]), ("LP3", A[:, 9] - A[:, 8]), ("VR+terms", A[:, 3] - A[:, 9])]
     for nm, v in sub:
         print("      wave0 %-12s median %8d  max %8d" % (nm, np.median(v), v.max()))
     cur = B[:, 0] >= t0                      # items of the last step only
