@@ -1290,9 +1290,12 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P, 
     if (may_consume && P.ok[e] && P.cc[e] == cc && P.rc[e] == rc) {
         if (lane < N) {
             const int64_t h = e * N + lane, EN = E * N;
-            en.hpx[lane] = P.h[h]; en.hpy[lane] = P.h[EN + h]; en.hgx[lane] = P.h[2 * EN + h];
-            en.hgy[lane] = P.h[3 * EN + h]; en.hr[lane] = P.h[4 * EN + h]; en.hvp[lane] = P.h[5 * EN + h];
-            en.hth[lane] = P.h[6 * EN + h];
+            double v[7];
+#pragma unroll
+            for (int f = 0; f < 7; ++f) v[f] = P.h[f * EN + h];
+            asm volatile("" ::: "memory");
+            en.hpx[lane] = v[0]; en.hpy[lane] = v[1]; en.hgx[lane] = v[2]; en.hgy[lane] = v[3];
+            en.hr[lane] = v[4]; en.hvp[lane] = v[5]; en.hth[lane] = v[6];
         }
         en.rpx = P.r[e]; en.rpy = P.r[E + e]; en.rgx = P.r[2 * E + e]; en.rgy = P.r[3 * E + e];
         const double rth = P.r[4 * E + e];
@@ -1476,30 +1479,38 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     int32_t pre_epl = 0, pre_sc = 0;
     uint32_t pre_ovf = 0;
     if (hl) {
+        // every load issued before the first LDS store (the compiler otherwise waits on each load in turn)
+        double hv[CN_HUM_F];
         pre_or = S.o_r[gh]; pre_vmax = S.o_vmax[gh]; pre_dm = S.o_dmask[gh];
-        HF(sl, H_PX, tid) = S.h_px[gh]; HF(sl, H_PY, tid) = S.h_py[gh];
-        HF(sl, H_GX, tid) = S.h_gx[gh]; HF(sl, H_GY, tid) = S.h_gy[gh];
-        HF(sl, H_VX, tid) = S.h_vx[gh]; HF(sl, H_VY, tid) = S.h_vy[gh];
-        HF(sl, H_R, tid) = S.h_r[gh]; HF(sl, H_VP, tid) = S.h_vpref[gh];
-        HF(sl, H_TH, tid) = S.h_theta[gh];
-        HF(sl, H_BPX, tid) = S.b_px[gh]; HF(sl, H_BPY, tid) = S.b_py[gh]; HF(sl, H_BVX, tid) = S.b_vx[gh];
-        HF(sl, H_BVY, tid) = S.b_vy[gh]; HF(sl, H_BR, tid) = S.b_r[gh];
+        hv[H_PX] = S.h_px[gh]; hv[H_PY] = S.h_py[gh]; hv[H_GX] = S.h_gx[gh]; hv[H_GY] = S.h_gy[gh];
+        hv[H_VX] = S.h_vx[gh]; hv[H_VY] = S.h_vy[gh]; hv[H_R] = S.h_r[gh]; hv[H_VP] = S.h_vpref[gh];
+        hv[H_TH] = S.h_theta[gh]; hv[H_BPX] = S.b_px[gh]; hv[H_BPY] = S.b_py[gh]; hv[H_BVX] = S.b_vx[gh];
+        hv[H_BVY] = S.b_vy[gh]; hv[H_BR] = S.b_r[gh];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int f = 0; f < CN_HUM_F; ++f) HF(sl, f, tid) = hv[f];
     }
     STAMP_A(12);
     if (rl) {
-        RF(sl, R_PX, re, EPB) = S.r_px[ge]; RF(sl, R_PY, re, EPB) = S.r_py[ge];
-        RF(sl, R_GX, re, EPB) = S.r_gx[ge]; RF(sl, R_GY, re, EPB) = S.r_gy[ge];
-        RF(sl, R_VX, re, EPB) = S.r_vx[ge]; RF(sl, R_VY, re, EPB) = S.r_vy[ge];
-        RF(sl, R_TH, re, EPB) = S.r_theta[ge]; RF(sl, R_RAD, re, EPB) = S.r_radius[ge];
-        RF(sl, R_VP, re, EPB) = S.r_vpref[ge]; RF(sl, R_POT, re, EPB) = S.potential[ge];
-        RF(sl, R_GT, re, EPB) = S.gtime[ge]; RF(sl, R_DV, re, EPB) = S.r_dv[ge];
-        sl.rflag[re] = S.flags[ge];
-        RF(sl, R_LAX, re, EPB) = S.last_ax[ge]; RF(sl, R_LAY, re, EPB) = S.last_ay[ge];
-        RF(sl, R_EPR, re, EPB) = S.ep_return[ge]; pre_epl = S.ep_len[ge];
-        pre_sc = S.scenario[ge]; pre_ovf = S.overflow[ge];
+        double rv[CN_RENV_F];
+        rv[R_PX] = S.r_px[ge]; rv[R_PY] = S.r_py[ge]; rv[R_GX] = S.r_gx[ge]; rv[R_GY] = S.r_gy[ge];
+        rv[R_VX] = S.r_vx[ge]; rv[R_VY] = S.r_vy[ge]; rv[R_TH] = S.r_theta[ge]; rv[R_RAD] = S.r_radius[ge];
+        rv[R_VP] = S.r_vpref[ge]; rv[R_POT] = S.potential[ge]; rv[R_GT] = S.gtime[ge]; rv[R_DV] = S.r_dv[ge];
+        rv[R_LAX] = S.last_ax[ge]; rv[R_LAY] = S.last_ay[ge]; rv[R_EPR] = S.ep_return[ge];
+        const uint32_t fl = S.flags[ge];
+        pre_epl = S.ep_len[ge]; pre_sc = S.scenario[ge]; pre_ovf = S.overflow[ge];
+        float a0 = g.actions[ge * 2], a1 = g.actions[ge * 2 + 1];
+        asm volatile("" ::: "memory");
+        RF(sl, R_PX, re, EPB) = rv[R_PX]; RF(sl, R_PY, re, EPB) = rv[R_PY];
+        RF(sl, R_GX, re, EPB) = rv[R_GX]; RF(sl, R_GY, re, EPB) = rv[R_GY];
+        RF(sl, R_VX, re, EPB) = rv[R_VX]; RF(sl, R_VY, re, EPB) = rv[R_VY];
+        RF(sl, R_TH, re, EPB) = rv[R_TH]; RF(sl, R_RAD, re, EPB) = rv[R_RAD];
+        RF(sl, R_VP, re, EPB) = rv[R_VP]; RF(sl, R_POT, re, EPB) = rv[R_POT];
+        RF(sl, R_GT, re, EPB) = rv[R_GT]; RF(sl, R_DV, re, EPB) = rv[R_DV];
+        RF(sl, R_LAX, re, EPB) = rv[R_LAX]; RF(sl, R_LAY, re, EPB) = rv[R_LAY]; RF(sl, R_EPR, re, EPB) = rv[R_EPR];
+        sl.rflag[re] = fl;
         STAMP_A(13);
         // ---- SRNN.clip_action (srnn.py:18-48) + unicycle integrator (crowd_sim_dict.py:211-217)
-        float a0 = g.actions[ge * 2], a1 = g.actions[ge * 2 + 1];
         if (holo) {
             const float n = np_norm2f(a0, a1);
             if ((double)n > RF(sl, R_VP, re, EPB)) {
