@@ -67,7 +67,7 @@ struct StepPlan {
     int rng_waves;   // phase-5 RNG regions (CN_PEND_LDS each), laid over o_lines
 };
 
-#define CN_RENV_F 17   // robot/env doubles per env in LDS
+#define CN_RENV_F 27   // robot/env doubles per env in LDS
 #define CN_HUM_F 14    // human doubles per lane in LDS
 #define CN_PEND_LDS (2 * CN_MT_N * 4 + 7 * 32 * 8 + 6 * 64 * 8)   // per RNG wave: MT ring, agent table, try slots
 
@@ -129,7 +129,9 @@ struct SL {
     uint8_t *ns;      // [M][T]
     uint8_t *perm;    // [A][T]
 };
-enum { R_PX, R_PY, R_GX, R_GY, R_VX, R_VY, R_TH, R_RAD, R_VP, R_POT, R_GT, R_DV, R_NX, R_NY, R_LAX, R_LAY, R_EPR };
+enum { R_PX, R_PY, R_GX, R_GY, R_VX, R_VY, R_TH, R_RAD, R_VP, R_POT, R_GT, R_DV, R_NX, R_NY, R_LAX, R_LAY, R_EPR,
+       // robot terms of calc_reward / kinematics computed early (phase 1), applied in phase 3
+       R_CVX, R_CVY, R_NTH, R_JERK, R_D2G, R_SPD, R_SL, R_SR, R_SEP, R_BITS };
 enum { H_PX, H_PY, H_GX, H_GY, H_VX, H_VY, H_R, H_VP, H_TH, H_BPX, H_BPY, H_BVX, H_BVY, H_BR };
 #define RF(sl, f, el, EPB) ((sl).r[(f) * (EPB) + (el)])
 #define HF(sl, f, t) ((sl).h[(f) * (sl).T + (t)])
@@ -1537,7 +1539,82 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     __syncthreads();
     STAMP_A(1);
 
+    // per-human terms of calc_reward (crowd_sim.py:934-969), PRE-move, for human lane hh
+    auto reward_terms = [&](int hh) {
+        const int elh = hh / N;
+        const double px = HF(sl, H_PX, hh), py = HF(sl, H_PY, hh);
+        const double vx0 = HF(sl, H_VX, hh), vy0 = HF(sl, H_VY, hh), rad = HF(sl, H_R, hh);
+        const double rdx = px - RF(sl, R_PX, elh, EPB), rdy = py - RF(sl, R_PY, elh, EPB);
+        sl.cd[hh] = dsqrt(rdx * rdx + rdy * rdy) - rad - RF(sl, R_RAD, elh, EPB);
+        double hcx[4], hcy[4], rcx[4], rcy[4];
+        vel_rect(px, py, vx0, vy0, rad, false, hcx, hcy);
+        for (int k = 0; k < 4; ++k) { rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh]; }
+        uint32_t f = quads_intersect(rcx, rcy, hcx, hcy) ? LF_VR : 0u;
+        if (!(np_norm2(px - HF(sl, H_GX, hh), py - HF(sl, H_GY, hh)) < rad)) f |= LF_NOTREACHED;
+        sl.lf[hh] = f;
+    };
+    // robot-only terms of calc_reward (crowd_sim.py:973-1030) and the robot's move (agent.py:172-212);
+    // independent of the humans, so the quad path computes them in phase 1 on wave 2
+    auto robot_terms = [&](int q) {
+        const int64_t gq = e0 + q;
+        const double rpx = RF(sl, R_PX, q, EPB), rpy = RF(sl, R_PY, q, EPB), rr = RF(sl, R_RAD, q, EPB);
+        const double rgx = RF(sl, R_GX, q, EPB), rgy = RF(sl, R_GY, q, EPB);
+        const bool rf32 = (sl.rflag[q] & CN_FLAG_ROBOT_F32) != 0;
+        const float a0 = sl.act[q], a1 = sl.act[EPB + q];
+        const bool reaching_goal = np_norm2(rpx - rgx, rpy - rgy) < rr;
+        // commanded world-frame velocity; unicycle: theta + r is float32 (NEP 50)
+        const float tr = (float)RF(sl, R_TH, q, EPB) + a1;
+        const float th_new = np_modf(tr, (float)(2 * CN_PI));
+        double cvx, cvy;
+        if (holo) { cvx = a0; cvy = a1; }
+        else { cvx = (double)(a0 * np_cosf(th_new)); cvy = (double)(a0 * np_sinf(th_new)); }
+        // unicycle differential drive (agent.py:185-194)
+        double upx = rpx, upy = rpy;
+        if (!holo && !(fabsf(a1) < 0.0001f)) {
+            const float w = fdiv(a1, (float)dt);
+            const float R = fdiv(a0, w);
+            const double th = RF(sl, R_TH, q, EPB);
+            double t1x, t1y;
+            if (rf32) { t1x = (double)(R * np_sinf((float)th)); t1y = (double)(R * np_cosf((float)th)); }
+            else { t1x = (double)R * sin(th); t1y = (double)R * cos(th); }
+            upx = rpx - t1x + (double)(R * np_sinf(tr));
+            upy = rpy + t1y - (double)(R * np_cosf(tr));
+        }
+        double side_l = 0, side_r = 0, sep = 0;
+        if (c.side_preference) {
+            const int eb = q * N;
+            double ex, ey;
+            if (holo) { ex = rpx + (double)(a0 * (float)dt); ey = rpy + (double)(a1 * (float)dt); }
+            else { ex = upx; ey = upy; }
+            const double hy = HF(sl, H_PY, eb), hr = HF(sl, H_R, eb);
+            if (ey <= hy + hr && ey >= hy - hr) { if (ex < HF(sl, H_PX, eb)) side_l = 1; else side_r = 1; }
+            sep = np_norm2(HF(sl, H_PX, eb) - rpx, HF(sl, H_PY, eb) - rpy);
+        }
+        {   // jerk (crowd_sim.py:1002-1009), float32 like the reference's np.float32 action
+            const float ax = (float)cvx - (float)RF(sl, R_VX, q, EPB), ay = (float)cvy - (float)RF(sl, R_VY, q, EPB);
+            const float dax = ax - (float)RF(sl, R_LAX, q, EPB), day = ay - (float)RF(sl, R_LAY, q, EPB);
+            RF(sl, R_JERK, q, EPB) = (double)(dax * dax + day * day);
+            S.last_ax[gq] = ax; S.last_ay[gq] = ay;
+        }
+        RF(sl, R_D2G, q, EPB) = np_norm2(rpx - rgx, rpy - rgy);
+        const bool inside = inside_world(rpx, rpy, rr, c.square_width / 2);
+        { const float fx = (float)cvx, fy = (float)cvy; RF(sl, R_SPD, q, EPB) = (double)fsqrt(fx * fx + fy * fy); }
+        RF(sl, R_SL, q, EPB) = side_l; RF(sl, R_SR, q, EPB) = side_r; RF(sl, R_SEP, q, EPB) = sep;
+        RF(sl, R_BITS, q, EPB) = (double)((reaching_goal ? 1u : 0u) | (inside ? 2u : 0u));
+        RF(sl, R_CVX, q, EPB) = cvx; RF(sl, R_CVY, q, EPB) = cvy; RF(sl, R_NTH, q, EPB) = th_new;
+        if (holo) {
+            RF(sl, R_NX, q, EPB) = rpx + (double)(a0 * (float)dt);
+            RF(sl, R_NY, q, EPB) = rpy + (double)(a1 * (float)dt);
+        } else { RF(sl, R_NX, q, EPB) = upx; RF(sl, R_NY, q, EPB) = upy; }
+    };
     // ---- phase 1: visibility of the other agents to human i, frozen simulator parameters --------
+    // (quad path: wave 1 computes the per-human reward terms, wave 2 the robot terms meanwhile)
+    if constexpr (!KD) {
+        if (tid >= 64 && tid - 64 < nenv_here * N) reward_terms(tid - 64);
+        if (tid >= 128 && tid - 128 < nenv_here) robot_terms(tid - 128);
+    } else {
+        if (rl) robot_terms(re);
+    }
     const bool orca = c.human_policy == CN_POLICY_ORCA;
     uint32_t vis = 0, dm = 0;
     float my_vmax = 0.0f;
@@ -1593,20 +1670,6 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
 
     // ---- phase 2: human policy (PRE-move state) + per-human reward terms -------------------------
     double nvx = 0.0, nvy = 0.0;
-    // per-human terms of calc_reward (crowd_sim.py:934-969), PRE-move, for human lane hh
-    auto reward_terms = [&](int hh) {
-        const int elh = hh / N;
-        const double px = HF(sl, H_PX, hh), py = HF(sl, H_PY, hh);
-        const double vx0 = HF(sl, H_VX, hh), vy0 = HF(sl, H_VY, hh), rad = HF(sl, H_R, hh);
-        const double rdx = px - RF(sl, R_PX, elh, EPB), rdy = py - RF(sl, R_PY, elh, EPB);
-        sl.cd[hh] = dsqrt(rdx * rdx + rdy * rdy) - rad - RF(sl, R_RAD, elh, EPB);
-        double hcx[4], hcy[4], rcx[4], rcy[4];
-        vel_rect(px, py, vx0, vy0, rad, false, hcx, hcy);
-        for (int k = 0; k < 4; ++k) { rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh]; }
-        uint32_t f = quads_intersect(rcx, rcy, hcx, hcy) ? LF_VR : 0u;
-        if (!(np_norm2(px - HF(sl, H_GX, hh), py - HF(sl, H_GY, hh)) < rad)) f |= LF_NOTREACHED;
-        sl.lf[hh] = f;
-    };
     if constexpr (!KD) {
         const int nh = nenv_here * N;
         if (orca) {
@@ -1707,8 +1770,6 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             else { nvx = nx; nvy = ny; }
             sl.nv[tid] = make_double2(nvx, nvy);
         }
-        // per-human reward terms on wave 1's lanes, beside their ORCA share
-        if (tid >= 64 && tid - 64 < nh) reward_terms(tid - 64);
         __syncthreads();
         if (hl) { nvx = sl.nv[tid].x; nvy = sl.nv[tid].y; }
     } else {
@@ -1890,12 +1951,10 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     __syncthreads();
     STAMP_A(3);
 
-    // ---- phase 3: calc_reward ladder + robot kinematics + Monitor (env lanes) ---------------------
+    // ---- phase 3: calc_reward ladder + Monitor (env lanes); the robot-only terms came from phase 1 --
     if (rl) {
-        const double rpx = RF(sl, R_PX, re, EPB), rpy = RF(sl, R_PY, re, EPB), rr = RF(sl, R_RAD, re, EPB);
-        const double rgx = RF(sl, R_GX, re, EPB), rgy = RF(sl, R_GY, re, EPB);
+        const double rr = RF(sl, R_RAD, re, EPB);
         const uint32_t flags = sl.rflag[re];
-        const bool rf32 = (flags & CN_FLAG_ROBOT_F32) != 0;
         const float a0 = sl.act[re], a1 = sl.act[EPB + re];
         const int eb = re * N;
         double dmin = INFINITY;
@@ -1909,55 +1968,20 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 nz_checked = true;
                 double zx[4], zy[4];
                 for (int z = 0; z < 2 && !nz_viol; ++z) {
-                    norm_zone(rpx, rpy, RF(sl, R_VX, re, EPB), RF(sl, R_VY, re, EPB), rr, rf32, c.norm_zone_lhs,
-                              z == 0, zx, zy);
-                    if (disc_quad_intersect(rpx, rpy, rr, zx, zy)) nz_viol = true;
+                    norm_zone(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB),
+                              RF(sl, R_VY, re, EPB), rr, (flags & CN_FLAG_ROBOT_F32) != 0, c.norm_zone_lhs, z == 0, zx,
+                              zy);
+                    if (disc_quad_intersect(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), rr, zx, zy)) nz_viol = true;
                 }
             }
             const uint32_t f = sl.lf[eb + k];
             vr_viol += (f & LF_VR) ? 1 : 0;
             agg += (f & LF_NOTREACHED) ? 1 : 0;
         }
-        const bool reaching_goal = np_norm2(rpx - rgx, rpy - rgy) < rr;
+        const uint32_t bits = (uint32_t)RF(sl, R_BITS, re, EPB);
+        const bool reaching_goal = (bits & 1u) != 0, inside = (bits & 2u) != 0;
         if (!reaching_goal) ++agg;
-        // commanded world-frame velocity; unicycle: theta + r is float32 (NEP 50)
-        const float tr = (float)RF(sl, R_TH, re, EPB) + a1;
-        const float th_new = np_modf(tr, (float)(2 * CN_PI));
-        double cvx, cvy;
-        if (holo) { cvx = a0; cvy = a1; }
-        else { cvx = (double)(a0 * np_cosf(th_new)); cvy = (double)(a0 * np_sinf(th_new)); }
-        // unicycle differential drive (agent.py:185-194)
-        double upx = rpx, upy = rpy;
-        if (!holo && !(fabsf(a1) < 0.0001f)) {
-            const float w = fdiv(a1, (float)dt);
-            const float R = fdiv(a0, w);
-            const double th = RF(sl, R_TH, re, EPB);
-            double t1x, t1y;
-            if (rf32) { t1x = (double)(R * np_sinf((float)th)); t1y = (double)(R * np_cosf((float)th)); }
-            else { t1x = (double)R * sin(th); t1y = (double)R * cos(th); }
-            upx = rpx - t1x + (double)(R * np_sinf(tr));
-            upy = rpy + t1y - (double)(R * np_cosf(tr));
-        }
-        double side_l = 0, side_r = 0, sep = 0;
-        if (c.side_preference) {
-            double ex, ey;
-            if (holo) { ex = rpx + (double)(a0 * (float)dt); ey = rpy + (double)(a1 * (float)dt); }
-            else { ex = upx; ey = upy; }
-            const double hy = HF(sl, H_PY, eb), hr = HF(sl, H_R, eb);
-            if (ey <= hy + hr && ey >= hy - hr) { if (ex < HF(sl, H_PX, eb)) side_l = 1; else side_r = 1; }
-            sep = np_norm2(HF(sl, H_PX, eb) - rpx, HF(sl, H_PY, eb) - rpy);
-        }
-        double jerk;
-        {
-            const float ax = (float)cvx - (float)RF(sl, R_VX, re, EPB), ay = (float)cvy - (float)RF(sl, R_VY, re, EPB);
-            const float dax = ax - (float)RF(sl, R_LAX, re, EPB), day = ay - (float)RF(sl, R_LAY, re, EPB);
-            jerk = (double)(dax * dax + day * day);
-            S.last_ax[ge] = ax; S.last_ay[ge] = ay;
-        }
-        const double dist_to_goal = np_norm2(rpx - rgx, rpy - rgy);
-        const bool inside = inside_world(rpx, rpy, rr, c.square_width / 2);
-        double speed;
-        { const float fx = (float)cvx, fy = (float)cvy; speed = (double)fsqrt(fx * fx + fy * fy); }
+        const double dist_to_goal = RF(sl, R_D2G, re, EPB);
         const double gt = RF(sl, R_GT, re, EPB);
         double reward;
         int done, event;
@@ -1987,25 +2011,21 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             info[CN_INFO_AGG_NAV_TIME] = (float)agg;
             info[CN_INFO_PATH_VIOLATION] = (float)vr_viol;
             info[CN_INFO_PERSONAL_VIOLATION] = dmin < c.min_personal_space ? 1.0f : 0.0f;
-            info[CN_INFO_JERK_COST] = (float)jerk;
+            info[CN_INFO_JERK_COST] = (float)RF(sl, R_JERK, re, EPB);
             info[CN_INFO_DIST_TO_GOAL] = (float)dist_to_goal;
-            info[CN_INFO_SPEED_VIOLATION] = speed > c.max_walking_speed ? 1.0f : 0.0f;
+            info[CN_INFO_SPEED_VIOLATION] = RF(sl, R_SPD, re, EPB) > c.max_walking_speed ? 1.0f : 0.0f;
             info[CN_INFO_MIN_DIST] = (float)dmin;
             info[CN_INFO_SCENARIO] = (float)pre_sc;
-            info[CN_INFO_SIDE_LEFT] = (float)side_l;
-            info[CN_INFO_SIDE_RIGHT] = (float)side_r;
-            info[CN_INFO_SEPARATION] = (float)sep;
+            info[CN_INFO_SIDE_LEFT] = (float)RF(sl, R_SL, re, EPB);
+            info[CN_INFO_SIDE_RIGHT] = (float)RF(sl, R_SR, re, EPB);
+            info[CN_INFO_SEPARATION] = (float)RF(sl, R_SEP, re, EPB);
             info[CN_INFO_OVERFLOW] = (float)pre_ovf;
         }
-        // robot kinematics (agent.py:198-212)
-        if (holo) {
-            RF(sl, R_NX, re, EPB) = rpx + (double)(a0 * (float)dt);
-            RF(sl, R_NY, re, EPB) = rpy + (double)(a1 * (float)dt);
-            RF(sl, R_VX, re, EPB) = a0; RF(sl, R_VY, re, EPB) = a1;
-        } else {
-            RF(sl, R_NX, re, EPB) = upx; RF(sl, R_NY, re, EPB) = upy;
-            RF(sl, R_TH, re, EPB) = th_new;
-            RF(sl, R_VX, re, EPB) = cvx; RF(sl, R_VY, re, EPB) = cvy;
+        // robot kinematics (agent.py:198-212): the post-move state computed in phase 1
+        if (holo) { RF(sl, R_VX, re, EPB) = a0; RF(sl, R_VY, re, EPB) = a1; }
+        else {
+            RF(sl, R_TH, re, EPB) = RF(sl, R_NTH, re, EPB);
+            RF(sl, R_VX, re, EPB) = RF(sl, R_CVX, re, EPB); RF(sl, R_VY, re, EPB) = RF(sl, R_CVY, re, EPB);
         }
         sl.rflag[re] = flags | CN_FLAG_ROBOT_F32;
         RF(sl, R_GT, re, EPB) = gt + dt;
