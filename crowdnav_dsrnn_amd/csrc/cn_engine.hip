@@ -102,7 +102,7 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_nd = o;    o = cn_align16(o + ML * (p.kd ? T : H) * 4);
     p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * T : 0));
     p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * T : 0));
-    p.rng_waves = p.kd ? T / 64 : 2;
+    p.rng_waves = p.kd ? T / 64 : 4;
     const int rng_end = p.o_lines + p.rng_waves * CN_PEND_LDS;
     p.total = o > rng_end ? o : rng_end;
     return p;
