@@ -63,11 +63,11 @@ def main():
         pmc[k] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": hbm}
         lines.append("%-40s FETCH_SIZE=%10.1f KiB  WRITE_SIZE=%10.1f KiB  HBM(2*fetch+write)=%12.0f B/launch" % (
             k[:40], f, w, hbm))
-    step = [k for k in pmc if k.startswith("cn_step_kernel")]
+    step = [k for k in pmc if "cn_step_kernel" in k]
     if step:
         d = dict(pmc[step[0]])
         d["kernel"] = step[0]
-        d["avg_duration_ns"] = next((v for n, v in avg.items() if n.startswith("cn_step_kernel")), None)
+        d["avg_duration_ns"] = next((v for n, v in avg.items() if "cn_step_kernel" in n), None)
         d["source"] = "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (%s)" % tag
         json.dump(d, open(os.path.join(HERE, "pmc_step_kernel.json"), "w"), indent=1)
     open(os.path.join(HERE, "%s_summary.txt" % tag), "w").write("\n".join(lines) + "\n")
