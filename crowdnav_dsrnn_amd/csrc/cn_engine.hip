@@ -1463,12 +1463,12 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     const int nenv_here = min(EPB, g.E - e0);
     const int el = tid / N, i = tid - el * N;
     const bool hl = el < nenv_here;               // human lane
-    const int64_t gh = (int64_t)(e0 + el) * N + i;  // global human index
+    const int gh = (e0 + el) * N + i;                 // global human index (E*N < 2^31, cn_config_validate)
     // env lanes (robot / reward / bookkeeping): wave 1 on the quad path, so they run beside the human
     // lanes of wave 0 in phases 0, 3 and 4; the first lanes on the kd-tree path
     const int re = KD ? tid : tid - 64;
     const bool rl = re >= 0 && re < nenv_here;
-    const int64_t ge = e0 + re;
+    const int ge = e0 + re;
     const bool holo = c.kinematics == CN_HOLONOMIC;
     const double dt = c.time_step;
 
@@ -2273,6 +2273,8 @@ int cn_config_validate(const cn_config *c)
 {
     if (!c) return set_err(CN_EINVAL, "null config");
     if (c->num_envs <= 0) return set_err(CN_EINVAL, "num_envs must be > 0");
+    if ((int64_t)c->num_envs * (c->human_num + 1) >= (1LL << 31) / 8)
+        return set_err(CN_EUNSUPPORTED, "num_envs * human_num too large for one engine (shard over engines)");
     if (c->human_num < 1 || c->human_num > 31) return set_err(CN_EUNSUPPORTED, "human_num must be in [1, 31]");
     if (c->human_num + (c->robot_visible ? 1 : 0) > CN_MAX_A) return set_err(CN_EUNSUPPORTED, "too many agents");
     if (c->num_scenarios < 1 || c->num_scenarios > CN_MAX_SCENARIOS) return set_err(CN_EINVAL, "num_scenarios");
