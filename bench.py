@@ -27,6 +27,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
+WORKLOAD_DESC = {
+    "c2": "C2: %d envs/GPU x %d humans, circle_crossing, ORCA humans (RVO2 f32), unicycle robot, dt=0.25, "
+          "actions U[-0.1,0.1]^2, auto-reset",
+    "c3": "C3: %d envs/GPU x %d humans, square_crossing, robot/human FOV pi, ORCA humans (kd-tree path), "
+          "holonomic robot, actions N(0,0.5^2), auto-reset",
+    "c5": "C5: %d envs/GPU (%s humans: traffic / side-preference halves), per-env scenario dispatch over "
+          "parallel/perpendicular traffic and the 3 side_pref scenarios, norm-zone reward, holonomic",
+}
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
 
@@ -36,16 +44,51 @@ def algorithmic_bytes_per_env_step(N):
     return 2 * (112 + 96 * N) + 8 + 4 * (9 + 2 * N) + 4 + 2
 
 
-def make_config(E, N, env_offset, nenv):
+def make_config(E, N, env_offset, nenv, workload="c2"):
+    """SURVEY.md §8d workloads. c2 (default, the BASELINE metric): circle_crossing, ORCA, unicycle.
+    c3: square_crossing ("random crossing"), robot/human FOV = pi, holonomic. c5 is two engines
+    (see engines_for)."""
     from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config
 
     c = clone_config(Config())
     c.sim.human_num = N
-    c.sim.train_val_sim = ["circle_crossing"]
-    c.sim.test_sim = ["circle_crossing"]
     c.humans.policy = "orca"
-    c.action_space.kinematics = "unicycle"
+    if workload == "c3":
+        c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
+        c.action_space.kinematics = "holonomic"
+        c.robot.FOV = c.humans.FOV = 1.0
+    else:
+        c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+        c.action_space.kinematics = "unicycle"
     return make_cn_config(c, num_envs=E, env_offset=env_offset, nenv=nenv, phase="train")
+
+
+def engines_for(workload, E, N, rank, world):
+    """(list of cn_config, per-engine action kind) for one rank. C5: per-env scenario
+    dispatch round-robin over {parallel, perpendicular} traffic (N = 5) and the three side-preference
+    scenarios (N = 1, circle radius 4, fixed robot), norm-zone reward and social metrics on: one engine
+    per human count, half of the envs each."""
+    from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config
+
+    if workload != "c5":
+        return [(make_config(E, N, rank * E, E * world, workload), workload)]
+    out = []
+    half = E // 2
+    for k, (scen, n) in enumerate(((["parallel_traffic", "perpendicular_traffic"], 5),
+                                   (["side_pref_passing", "side_pref_overtaking", "side_pref_crossing"], 1))):
+        c = clone_config(Config())
+        c.sim.train_val_sim = c.sim.test_sim = scen
+        c.sim.human_num = n
+        c.humans.policy = "orca"
+        c.action_space.kinematics = "holonomic"
+        c.reward.norm_zones = True
+        if n == 1:
+            c.test.side_preference = True
+            c.sim.circle_radius = 4
+            c.humans.random_goal_changing = False
+            c.humans.end_goal_changing = False
+        out.append((make_cn_config(c, num_envs=half, env_offset=rank * half, nenv=half * world, phase="train"), "c5"))
+    return out
 
 
 def cpu_baseline(N, budget_s=12.0):
@@ -92,6 +135,8 @@ def main():
     ap.add_argument("--humans", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
+                    help="c2 = BASELINE metric (default); c3 / c5 are the SURVEY §8d side measurements")
     args = ap.parse_args()
 
     import torch
@@ -112,14 +157,26 @@ def main():
     from crowdnav_dsrnn_amd.engine import CrowdNavEngine
 
     E, N, K, W = args.envs, args.humans, args.steps, args.warmup
-    cfg = make_config(E, N, env_offset=rank * E, nenv=E * world)
-    eng = CrowdNavEngine(cfg, device)
+    if args.workload == "c3" and N == 10:
+        N = 25
+    if args.workload == "c5" and E == 4096:
+        E = 8192
+    engs = [CrowdNavEngine(cfg, device) for cfg, _ in engines_for(args.workload, E, N, rank, world)]
+    eng = engs[0]
     gen = torch.Generator(device=device)
     gen.manual_seed(rank)
-    actions = (torch.rand((K + W, E, 2), generator=gen, device=device) * 0.2 - 0.1).contiguous()
-    eng.reset()
+    acts = []
+    for e_ in engs:
+        if args.workload == "c2":   # unicycle (dv, dtheta) ~ U[-0.1, 0.1]^2
+            a = torch.rand((K + W, e_.E, 2), generator=gen, device=device) * 0.2 - 0.1
+        else:                       # holonomic (vx, vy) ~ N(0, 0.5^2), clipped by clip_action in the kernel
+            a = torch.randn((K + W, e_.E, 2), generator=gen, device=device) * 0.5
+        acts.append(a.contiguous())
+    for e_ in engs:
+        e_.reset()
     for s in range(W):
-        eng.step(actions[s])
+        for e_, a in zip(engs, acts):
+            e_.step(a[s])
     L = _lib.lib()
 
     def barrier():
@@ -132,7 +189,8 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for s in range(K):
-        eng.step(actions[W + s])
+        for e_, a in zip(engs, acts):
+            e_.step(a[W + s])
     barrier()
     elapsed = time.perf_counter() - t0
     a_ms, b_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
@@ -144,12 +202,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    E_total = sum(e_.E for e_ in engs)
     if rank == 0:
-        value = world * E * K / elapsed
+        value = world * E_total * K / elapsed
         kernel_s = a_ms.value / 1e3 / max(n.value, 1)
-        bpl = algorithmic_bytes_per_env_step(N) * E
+        bpl = algorithmic_bytes_per_env_step(eng.N) * eng.E   # the timed kernel is engs[0]'s
         achieved = bpl / kernel_s / 1e9
-        traffic = load_pmc_traffic()
+        traffic = load_pmc_traffic() if args.workload == "c2" else None
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -164,9 +223,9 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": "C2: %d envs/GPU x %d humans, circle_crossing, ORCA humans (RVO2 f32), unicycle robot, "
-                            "dt=0.25, actions U[-0.1,0.1]^2, auto-reset" % (E, N),
-                "envs_per_gpu": E, "humans": N, "global_envs": E * world,
+                "workload": WORKLOAD_DESC[args.workload] % (E_total, N),
+                "envs_per_gpu": E_total, "humans": N if args.workload != "c5" else "5 / 1",
+                "global_envs": E_total * world,
                 "parallelism": "env-sharded x%d (no collective)" % world,
                 "step_kernel_ms": round(kernel_s * 1e3, 5),
             },
@@ -181,10 +240,11 @@ def main():
                 "algorithmic_bytes_per_launch": bpl,
             },
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.workload == "c2":
             line["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
         print(json.dumps(line), flush=True)
-    eng.close()
+    for e_ in engs:
+        e_.close()
     if dist is not None:
         dist.destroy_process_group()
 

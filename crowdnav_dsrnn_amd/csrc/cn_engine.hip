@@ -875,32 +875,52 @@ __device__ __forceinline__ bool goal_hit(const cn_config &c, const Env1 &en, int
     return norm_lt(gx - ax, gy - ay, md) || norm_lt(gx - agx, gy - agy, md);
 }
 
-// Rejection loop of the reference (`while True: draw; if not collide: break`) with the tries AND the
-// agent tests spread over the wave: lane = (try t, agent a), t = lane / NA, a = lane % NA, so
-// J = 64 / NA consecutive tries are evaluated per pass (each try consumes W words, so try t's words
-// start at p + W*t). `cand(q, t)` runs on the a == 0 lane of each try and leaves the candidate in slot
-// t of m.sl; `hit(t, a)` is one agent test (true = collision). The first try without a hit wins, as
-// in the reference. Bounded by max_tries (the reference loops forever; after max_tries the last try
-// is accepted and `ovf` counts it). Returns the winning slot; m.p is after its words.
+// Rejection loop of the reference (`while True: draw; if not collide: break`), speculative over the
+// wave. Each try consumes W words, so try t's words start at p + W*t. The first pass spreads the tries
+// AND the agent tests: lane = (try t, agent a), t = lane / NA, a = lane % NA, J = 64 / NA tries; later
+// passes (crowded scenes, where early tries keep failing) put one try per lane, 64 per pass, each lane
+// testing the agents in turn. `cand(q, t)` leaves try t's candidate in slot t of m.sl; `hit(t, a)` is
+// one agent test (true = collision). The first try without a hit wins, as in the reference. Bounded by
+// max_tries (the reference loops forever; after max_tries the last try is accepted and `ovf` counts
+// it). Returns the winning slot; m.p is after its words.
 template <typename FC, typename FT>
 __device__ int wave_reject2(WRng &m, int W, int NA, int max_tries, uint32_t &ovf, FC cand, FT hit)
 {
     const int lane = m.lane;
-    const int J = min(64 / NA, CN_MT_N / W);
-    const int t = lane / NA, a = lane - t * NA;
     const uint64_t gmask = NA >= 64 ? ~0ull : ((1ull << NA) - 1ull);
-    for (int t0 = 0;; t0 += J) {
+    int t0 = 0;
+    {   // first pass, lane = (try, agent): the common case (an early try is accepted) in one short pass
+        const int J = min(64 / NA, CN_MT_N / W);
+        const int t = lane / NA, a = lane - t * NA;
         m.ensure(W * J);
-        const int nt = min(J, max_tries - t0);
+        const int nt = min(J, max_tries);
         const bool valid = t < nt;
         if (valid && a == 0) cand(m.p + W * t, t);
         wsync();
-        const bool bad = valid && hit(t, a);
-        const uint64_t badm = __ballot(bad);
-        int first = -1;
+        const uint64_t badm = __ballot(valid && hit(t, a));
         for (int k = 0; k < nt; ++k)
-            if (((badm >> (k * NA)) & gmask) == 0) { first = k; break; }
-        if (first >= 0) { m.p += W * (first + 1); return first; }
+            if (((badm >> (k * NA)) & gmask) == 0) { m.p += W * (k + 1); return k; }
+        if (J >= max_tries) { m.p += W * nt; ++ovf; return nt - 1; }
+        m.p += W * J;
+        t0 = J;
+        wsync();
+    }
+    // crowded: lane = try (64 per pass), each lane tests the agents in turn
+    const int J = min(64, CN_MT_N / W);
+    for (;; t0 += J) {
+        m.ensure(W * J);
+        const int nt = min(J, max_tries - t0);
+        const bool valid = lane < nt;
+        if (valid) cand(m.p + W * lane, lane);
+        wsync();
+        bool bad = !valid;
+        for (int a = 0; a < NA && !bad; ++a) bad = hit(lane, a);
+        const uint64_t okm = __ballot(!bad);
+        if (okm) {
+            const int first = __ffsll((long long)okm) - 1;
+            m.p += W * (first + 1);
+            return first;
+        }
         if (t0 + J >= max_tries) { m.p += W * nt; ++ovf; return nt - 1; }
         m.p += W * J;
         wsync();   // slots are rewritten by the next pass

@@ -25,6 +25,12 @@ def run(variant, E=4096, N=10, steps=300):
         c.humans.end_goal_changing = False
     if variant == "sf":
         c.humans.policy = "social_force"
+    if variant == "c3":
+        N = 25
+        c.sim.human_num = N
+        c.sim.train_val_sim = ["square_crossing"]
+        c.action_space.kinematics = "holonomic"
+        c.robot.FOV = c.humans.FOV = 1.0
     eng = CrowdNavEngine(make_cn_config(c, num_envs=E), "cuda:0")
     eng.reset()
     L = _lib.lib()
