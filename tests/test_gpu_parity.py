@@ -51,15 +51,82 @@ def test_gpu_rollout_vs_reference(gpu, name):
     assert not errs, "\n".join(errs[:20])
 
 
-def _cfg(N=10, kin="unicycle", scen="circle_crossing", policy="orca", E=256, fov=2.0):
+def _cfg(N=10, kin="unicycle", scen="circle_crossing", policy="orca", E=256, fov=2.0, **over):
     c = clone_config(Config())
     c.sim.human_num = N
     c.action_space.kinematics = kin
-    c.sim.train_val_sim = [scen]
+    c.sim.train_val_sim = list(scen) if isinstance(scen, (list, tuple)) else [scen]
+    c.sim.test_sim = c.sim.train_val_sim
     c.humans.policy = policy
     c.robot.FOV = fov
     c.humans.FOV = fov
+    for k, v in over.items():   # "section__field": value
+        sec, fld = k.split("__")
+        setattr(getattr(c, sec), fld, v)
+    if c.test.side_preference:
+        c.humans.random_goal_changing = False
+        c.humans.end_goal_changing = False
     return make_cn_config(c, num_envs=E)
+
+
+def _teacher_forced(gpu, oracle, cfg, kin, steps=60, seed=5):
+    """Norm zones (parity unpinned): the robot's own disc exactly touches a zone corner, so
+    the -0.5 penalty flips with last-ulp differences of the rotation (GPU ocml vs glibc trig); env-steps
+    whose reward differs by exactly the penalty are excluded from the reward / ep_return comparison,
+    and must stay below 1 % of env-steps."""
+    ref = oracle.RefEngine(cfg)
+    g = gpu(cfg)
+    ref.reset()
+    rng = np.random.RandomState(seed)
+    mism = flips = 0
+    for t in range(steps):
+        a = (rng.uniform(-0.15, 0.15, (cfg.num_envs, 2)) if kin == "unicycle"
+             else rng.normal(0, 0.8, (cfg.num_envs, 2))).astype(np.float32)
+        g.set_state(ref.get_state())
+        r_out = ref.step(a)
+        g_out = g.step(a)
+        rs, gs = ref.get_state(), g.get_state()
+        np.testing.assert_array_equal(g_out[2], r_out[2], err_msg="done t=%d" % t)
+        np.testing.assert_array_equal(g_out[3], r_out[3], err_msg="event t=%d" % t)
+        keep = np.ones(cfg.num_envs, bool)
+        if cfg.norm_zones:
+            dr = np.abs(g_out[1].astype(np.float64) - r_out[1])
+            flip = np.abs(dr - abs(cfg.norm_zone_penalty)) < 1e-5
+            flips += int(flip.sum())
+            keep = ~flip
+        np.testing.assert_allclose(g_out[1][keep], r_out[1][keep], atol=1e-5, rtol=0, err_msg="reward t=%d" % t)
+        for k in ("robot_node", "temporal_edges", "spatial_edges"):
+            np.testing.assert_allclose(g_out[0][k], r_out[0][k], atol=1e-5, rtol=0, err_msg="%s t=%d" % (k, t))
+        d = {"post_" + n: np.asarray(getattr(rs, n)) for n, _, _ in abi.STATE_FIELDS if n != "mt"}
+        d["post_mt_crc"] = H.mt_crc(rs)
+        errs = H.compare_state(gs, d, "post_", tol=1e-5, where="t=%d " % t, skip=("ep_return",))
+        errs += H.compare_state(gs, {"post_ep_return": d["post_ep_return"]}, "post_", tol=1e-5, env_mask=keep,
+                                where="t=%d " % t)
+        assert not errs, errs
+        mism += int((g_out[4][:, abi.INFO_PATH_VIOLATION] != r_out[4][:, abi.INFO_PATH_VIOLATION]).sum())
+    assert mism <= cfg.num_envs * steps * 0.001, mism
+    assert flips <= cfg.num_envs * steps * 0.01, flips
+
+
+@pytest.mark.parametrize("name,kin,N,policy,scen,over", [
+    ("c5_traffic_normzones", "holonomic", 5, "orca", ("parallel_traffic", "perpendicular_traffic"),
+     {"reward__norm_zones": True}),
+    ("c5_side_pref", "holonomic", 1, "orca", ("side_pref_passing", "side_pref_overtaking", "side_pref_crossing"),
+     {"test__side_preference": True, "sim__circle_radius": 4}),
+    ("social_metrics_sequential", "holonomic", 5, "orca",
+     ("parallel_traffic", "perpendicular_traffic", "circle_crossing", "square_crossing"),
+     {"test__social_metrics": True, "sim__circle_radius": 4}),
+    ("robot_visible_quad", "unicycle", 9, "orca", "circle_crossing", {"robot__visible": True}),
+    ("random_radii_vpref", "holonomic", 6, "orca", "circle_crossing",
+     {"humans__random_radii": True, "humans__random_v_pref": True}),
+    ("unicycle_sf_perp", "unicycle", 5, "social_force", "perpendicular_traffic", {}),
+    ("single_human", "holonomic", 1, "orca", "circle_crossing", {}),
+    ("two_humans_time_factor", "unicycle", 2, "orca", "circle_crossing", {"reward__time_factor": True}),
+])
+def test_gpu_vs_oracle_configs(gpu, oracle, name, kin, N, policy, scen, over):
+    """Teacher-forced GPU vs oracle over the option space the reference exposes (SURVEY §8d C5 shapes,
+    norm zones, side preference, social-metrics scenario order, visible robot, radius/v_pref jitter)."""
+    _teacher_forced(gpu, oracle, _cfg(N, kin, scen, policy, 256, 2.0, **over), kin)
 
 
 @pytest.mark.parametrize("kin,N,policy,scen,fov", [
