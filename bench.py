@@ -32,6 +32,8 @@ WORKLOAD_DESC = {
           "actions U[-0.1,0.1]^2, auto-reset",
     "c3": "C3: %d envs/GPU x %d humans, square_crossing, robot/human FOV pi, ORCA humans (kd-tree path), "
           "holonomic robot, actions N(0,0.5^2), auto-reset",
+    "c4": "C4: %d envs/GPU x %d humans, circle_crossing, ORCA humans, holonomic robot, DSRNN act() in the loop "
+          "(sampled actions), PPO num_steps=128 epochs=5 minibatches=2, grads all-reduced over RCCL",
     "c5": "C5: %d envs/GPU (%s humans: traffic / side-preference halves), per-env scenario dispatch over "
           "parallel/perpendicular traffic and the 3 side_pref scenarios, norm-zone reward, holonomic",
 }
@@ -126,6 +128,83 @@ def load_pmc_traffic():
         return None
 
 
+def run_c4(args, torch, dist, device, rank, world):
+    """env-steps/s over PPO updates, counted like train.py:342-352 (rollout of num_steps
+    steps of every env with DSRNN act() in the loop, then the PPO update, all inside the timed region).
+    A "step" here is one update = 128 x E env steps per GPU. Defaults: 10 timed updates, 1 warmup."""
+    from crowdnav_dsrnn_amd.config import Config, clone_config
+    from crowdnav_dsrnn_amd.envs import CrowdNavVecEnv
+    from crowdnav_dsrnn_amd.learner import PPO
+    from crowdnav_dsrnn_amd.learner.loop import RolloutTrainer
+    from crowdnav_dsrnn_amd.policy import Policy
+
+    E, N = args.envs, args.humans
+    K = args.steps if args.steps != 2000 else 10
+    W = args.warmup if args.warmup != 100 else 1
+    c = clone_config(Config())
+    c.sim.human_num = N
+    c.humans.policy = "orca"
+    c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+    c.action_space.kinematics = "holonomic"
+    c.training.num_processes = E
+    c.ppo.num_steps = 128
+    c.ppo.epoch = 5
+    c.ppo.num_mini_batch = 2
+    c.training.lr = 4e-5
+    c.training.eps = 1e-5
+    c.training.max_grad_norm = 0.5
+    torch.manual_seed(0)
+    envs = CrowdNavVecEnv(c, E, c.env.seed, device, env_offset=rank * E, nenv=E * world)
+    pol = Policy(envs.observation_space.spaces, envs.action_space, base="srnn", base_kwargs=c).to(device)
+    agent = PPO(pol, c.ppo.clip_param, c.ppo.epoch, c.ppo.num_mini_batch, c.ppo.value_loss_coef,
+                c.ppo.entropy_coef, lr=c.training.lr, eps=c.training.eps, max_grad_norm=c.training.max_grad_norm)
+    tr = RolloutTrainer(c, envs, pol, agent)
+
+    def barrier():
+        torch.cuda.synchronize(device)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    for _ in range(W):
+        tr.update()
+    barrier()
+    t0 = time.perf_counter()
+    roll = upd = 0.0
+    for _ in range(K):
+        st = tr.update()
+        roll += st["rollout_s"]
+        upd += st["update_s"]
+        if rank == 0:
+            print("c4 update: rollout %.3f s, ppo %.3f s, episodes %d, mean return %.3f, value_loss %.4f"
+                  % (st["rollout_s"], st["update_s"], st["episodes"], st["mean_episode_return"],
+                     st["value_loss"]), file=sys.stderr, flush=True)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        steps_per_update = c.ppo.num_steps * E
+        line = {
+            "metric": METRIC + " [C4 side measurement: incl. DSRNN act + PPO update]",
+            "value": round(world * steps_per_update * K / elapsed, 1),
+            "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
+            "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64 env / fp32 policy", "data": "synthetic",
+            "config": {"workload": WORKLOAD_DESC["c4"] % (E, N), "envs_per_gpu": E, "humans": N,
+                       "global_envs": E * world, "env_steps_per_update": steps_per_update * world,
+                       "rollout_s_per_update": round(roll / K, 4), "ppo_s_per_update": round(upd / K, 4),
+                       "parallelism": "dp%d (env-sharded, PPO grads all-reduced)" % world},
+            "roofline": None,
+        }
+        print(json.dumps(line), flush=True)
+    envs.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,8 +214,9 @@ def main():
     ap.add_argument("--humans", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2",
-                    help="c2 = BASELINE metric (default); c3 / c5 are the SURVEY §8d side measurements")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2 = BASELINE metric (default); c3 / c4 / c5 are the SURVEY §8d side measurements "
+                         "(c4: --steps / --warmup count PPO updates)")
     args = ap.parse_args()
 
     import torch
@@ -157,6 +237,8 @@ def main():
     from crowdnav_dsrnn_amd.engine import CrowdNavEngine
 
     E, N, K, W = args.envs, args.humans, args.steps, args.warmup
+    if args.workload == "c4":
+        return run_c4(args, torch, dist, device, rank, world)
     if args.workload == "c3" and N == 10:
         N = 25
     if args.workload == "c5" and E == 4096:

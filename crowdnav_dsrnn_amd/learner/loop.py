@@ -1,0 +1,73 @@
+"""Device-resident rollout + PPO loop: the body of the reference's train.py:219-330, without host
+round trips per step (train.py moves actions to the CPU, builds masks from Python lists and walks the
+infos of every env at every step).
+
+    trainer = RolloutTrainer(config, envs, actor_critic, agent)
+    stats = trainer.update()      # num_steps env steps of every env + one PPO update
+
+`envs` is a crowdnav_dsrnn_amd.envs.CrowdNavVecEnv (step_device path); episode returns are read from the
+engine's Monitor counters where `done`.
+"""
+import time
+
+import torch
+
+from .storage import SRNNRolloutStorage
+
+
+class RolloutTrainer:
+    def __init__(self, config, envs, actor_critic, agent, deterministic=False):
+        self.config = config
+        self.envs = envs
+        self.ac = actor_critic
+        self.agent = agent
+        self.deterministic = deterministic
+        dev = envs.engine.device
+        self.device = dev
+        self.rollouts = SRNNRolloutStorage(config.ppo.num_steps, envs.num_envs, envs.observation_space.spaces,
+                                           envs.action_space, config.SRNN.human_node_rnn_size,
+                                           config.SRNN.human_human_edge_rnn_size, "GRU", device=dev,
+                                           compact_hidden=True)
+        obs = envs.reset()
+        for k in self.rollouts.obs:
+            self.rollouts.obs[k][0].copy_(obs[k])
+        self.episode_returns = []
+        self.env_steps = 0
+
+    @torch.no_grad()
+    def collect(self):
+        r = self.rollouts
+        ep_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        ep_cnt = torch.zeros((), dtype=torch.int64, device=self.device)
+        for step in range(r.num_steps):
+            obs_s = {k: v[step] for k, v in r.obs.items()}
+            hxs_s = r.hidden(step)
+            value, action, logp, hxs = self.ac.act(obs_s, hxs_s, r.masks[step], deterministic=self.deterministic)
+            obs, reward, done, _, _, ep_ret, _ = self.envs.step_device(action)
+            masks = (1.0 - done.float()).unsqueeze(1)
+            r.insert(obs, hxs, action, logp, value, reward.unsqueeze(1), masks, torch.ones_like(masks))
+            d = done.bool()
+            ep_sum += torch.where(d, ep_ret, torch.zeros_like(ep_ret)).sum()
+            ep_cnt += d.sum()
+        self.env_steps += r.num_steps * self.envs.num_envs
+        return ep_sum, ep_cnt
+
+    def update(self):
+        t0 = time.perf_counter()
+        ep_sum, ep_cnt = self.collect()
+        r = self.rollouts
+        with torch.no_grad():
+            next_value = self.ac.get_value({k: v[-1] for k, v in r.obs.items()},
+                                           r.hidden(r.num_steps),
+                                           r.masks[-1]).detach()
+        c = self.config
+        r.compute_returns(next_value, c.ppo.use_gae, c.reward.gamma, c.ppo.gae_lambda,
+                          c.training.use_proper_time_limits)
+        t1 = time.perf_counter()
+        losses = self.agent.update(r)
+        r.after_update()
+        t2 = time.perf_counter()
+        n = int(ep_cnt.item())
+        return {"value_loss": losses[0], "action_loss": losses[1], "dist_entropy": losses[2],
+                "episodes": n, "mean_episode_return": float(ep_sum.item()) / max(n, 1),
+                "rollout_s": t1 - t0, "update_s": t2 - t1}

@@ -12,6 +12,8 @@ oracle/shims (gym, shapely, rvo2, torchvision — see oracle/shims/README.md) an
                  (shmem_vec_env.py:164-168) and bench.Monitor's episode return
   dsrnn.npz      DSRNN Policy.act / evaluate_actions with procedural weights
                  (pytorchBaselines/a2c_ppo_acktr/model.py:63-104, srnn_model.py:409-504)
+  ppo.npz        SRNNRolloutStorage + compute_returns + PPO.update on procedural weights
+                 (pytorchBaselines/a2c_ppo_acktr/storage.py:14-292, algo/ppo.py:36-118)
 
 The fixtures are data only (inputs and expected outputs); nothing of the reference's source is
 copied. The reference never travels to the GPU box; these .npz files do.
@@ -455,6 +457,76 @@ def gen_dsrnn(outdir):
     print("dsrnn ok")
 
 
+def gen_ppo(outdir):
+    """SRNNRolloutStorage.insert / compute_returns / recurrent_generator + PPO.update of the reference
+    (pytorchBaselines/a2c_ppo_acktr/storage.py:14-292, algo/ppo.py:36-118) on procedural DSRNN weights:
+    inputs, the returns and the parameters after one update (torch RNG seeded before the update, so the
+    minibatch permutation is reproducible)."""
+    import torch
+
+    torch.set_num_threads(4)
+    import gym
+    from pytorchBaselines.a2c_ppo_acktr import algo
+    from pytorchBaselines.a2c_ppo_acktr.model import Policy
+    from pytorchBaselines.a2c_ppo_acktr.storage import SRNNRolloutStorage
+
+    out = {}
+    N, E, T = 5, 4, 8
+    cfg = make_ref_config(N=N)
+    cfg.training.cuda = False
+    cfg.training.num_processes = E
+    cfg.ppo.num_steps = T
+    cfg.ppo.num_mini_batch = 2
+    obs_space = {"robot_node": gym.spaces.Box(-np.inf, np.inf, (1, 7)),
+                 "temporal_edges": gym.spaces.Box(-np.inf, np.inf, (1, 2)),
+                 "spatial_edges": gym.spaces.Box(-np.inf, np.inf, (N, 2))}
+    act_space = gym.spaces.Box(-np.inf, np.inf, (2,))
+    torch.manual_seed(0)
+    pol = Policy(obs_space, act_space, base="srnn", base_kwargs=cfg)
+    pol.load_state_dict(procedural_state_dict(pol))
+    rol = SRNNRolloutStorage(T, E, obs_space, act_space, 128, 256, recurrent_cell_type="GRU")
+    rng = np.random.RandomState(31)
+
+    def rnd(*shape, s=1.0):
+        return rng.normal(0, s, shape).astype(np.float32)
+
+    obs0 = {"robot_node": rnd(E, 1, 7, s=3), "temporal_edges": rnd(E, 1, 2, s=0.5), "spatial_edges": rnd(E, N, 2, s=4)}
+    for k, v in obs0.items():
+        rol.obs[k][0].copy_(torch.from_numpy(v))
+        out["obs0_" + k] = v
+    ins = []
+    for t in range(T):
+        d = {"obs_robot_node": rnd(E, 1, 7, s=3), "obs_temporal_edges": rnd(E, 1, 2, s=0.5),
+             "obs_spatial_edges": rnd(E, N, 2, s=4),
+             "hxs_human_node_rnn": rnd(E, 1, 128, s=0.3), "hxs_human_human_edge_rnn": rnd(E, N + 1, 256, s=0.3),
+             "actions": rnd(E, 2, s=0.5), "logp": rnd(E, 1), "values": rnd(E, 1), "rewards": rnd(E, 1),
+             "masks": (rng.uniform(size=(E, 1)) > 0.2).astype(np.float32),
+             "bad_masks": (rng.uniform(size=(E, 1)) > 0.1).astype(np.float32)}
+        rol.insert({k[4:]: torch.from_numpy(d[k]) for k in d if k.startswith("obs_")},
+                   {k[4:]: torch.from_numpy(d[k]) for k in d if k.startswith("hxs_")},
+                   torch.from_numpy(d["actions"]), torch.from_numpy(d["logp"]), torch.from_numpy(d["values"]),
+                   torch.from_numpy(d["rewards"]), torch.from_numpy(d["masks"]), torch.from_numpy(d["bad_masks"]))
+        for k, v in d.items():
+            out["t%d_%s" % (t, k)] = v
+    next_value = rnd(E, 1)
+    out["next_value"] = next_value
+    rol.compute_returns(torch.from_numpy(next_value), True, 0.99, 0.95, True)
+    out["returns_gae_ptl"] = rol.returns.numpy().copy()
+    agent = algo.PPO(pol, 0.2, 2, 2, 0.5, 0.01, lr=4e-5, eps=1e-5, max_grad_norm=0.5)
+    torch.manual_seed(1234)
+    vl, al, de = agent.update(rol)
+    out["update_losses"] = np.array([vl, al, de])
+    for k, v in pol.state_dict().items():
+        out["param_" + k] = v.numpy().copy()
+    # the other compute_returns branches on the same data
+    for use_gae, ptl, name in ((False, True, "returns_nogae_ptl"), (True, False, "returns_gae"),
+                               (False, False, "returns_nogae")):
+        rol.compute_returns(torch.from_numpy(next_value), use_gae, 0.99, 0.95, ptl)
+        out[name] = rol.returns.numpy().copy()
+    np.savez_compressed(os.path.join(outdir, "ppo.npz"), **out)
+    print("ppo ok")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
@@ -515,6 +587,8 @@ def main():
             signal.alarm(0)
     if want("dsrnn"):
         gen_dsrnn(args.out)
+    if want("ppo"):
+        gen_ppo(args.out)
 
 
 if __name__ == "__main__":

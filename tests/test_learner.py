@@ -1,0 +1,175 @@
+"""On-device PPO learner vs the reference (tests/golden/ppo.npz: the reference's SRNNRolloutStorage +
+compute_returns + PPO.update on procedural DSRNN weights, pytorchBaselines/a2c_ppo_acktr/storage.py,
+algo/ppo.py). Same seeded minibatch permutation (torch.randperm on the default generator).
+Tolerances: returns 1e-6 (same fp32 operation order); losses / parameters after one update 2e-6 / 1e-6
+absolute on CPU (fp32 GEMM/GRU summation order), 5e-5 / 5e-6 on the GPU."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from crowdnav_dsrnn_amd.learner import PPO, SRNNRolloutStorage
+from crowdnav_dsrnn_amd.spaces import Box
+from tests.helpers import edge_features_fp32, load, make_policy
+
+N, E, T = 5, 4, 8
+
+
+@pytest.fixture(scope="module")
+def fx():
+    return load("ppo.npz")
+
+
+def _spaces():
+    return {"robot_node": Box(-np.inf, np.inf, (1, 7)), "temporal_edges": Box(-np.inf, np.inf, (1, 2)),
+            "spatial_edges": Box(-np.inf, np.inf, (N, 2))}, Box(-np.inf, np.inf, (2,))
+
+
+def _filled(fx, device="cpu", compact=False):
+    obs_sp, act_sp = _spaces()
+    rol = SRNNRolloutStorage(T, E, obs_sp, act_sp, 128, 256, "GRU", device=device, compact_hidden=compact)
+    for k in rol.obs:
+        rol.obs[k][0].copy_(torch.from_numpy(fx["obs0_" + k]))
+    for t in range(T):
+        g = lambda n: torch.from_numpy(fx["t%d_%s" % (t, n)]).to(device)  # noqa: E731
+        rol.insert({k: g("obs_" + k) for k in rol.obs}, {k: g("hxs_" + k) for k in rol.recurrent_hidden_states},
+                   g("actions"), g("logp"), g("values"), g("rewards"), g("masks"), g("bad_masks"))
+    return rol
+
+
+@pytest.mark.parametrize("use_gae,ptl,key", [(True, True, "returns_gae_ptl"), (False, True, "returns_nogae_ptl"),
+                                             (True, False, "returns_gae"), (False, False, "returns_nogae")])
+def test_compute_returns(fx, use_gae, ptl, key):
+    rol = _filled(fx)
+    rol.compute_returns(torch.from_numpy(fx["next_value"]), use_gae, 0.99, 0.95, ptl)
+    # returns[-1] is only written by the non-GAE branches (the fixture ran the branches in sequence)
+    np.testing.assert_allclose(rol.returns.numpy()[:-1], fx[key][:-1], atol=1e-6, rtol=0)
+    if not use_gae:
+        np.testing.assert_allclose(rol.returns.numpy()[-1], fx[key][-1], atol=0, rtol=0)
+
+
+def test_recurrent_generator_layout(fx):
+    rol = _filled(fx)
+    adv = torch.arange(T * E, dtype=torch.float32).reshape(T, E, 1)
+    torch.manual_seed(7)
+    perm = torch.randperm(E)
+    torch.manual_seed(7)
+    batches = list(rol.recurrent_generator(adv, 2))
+    assert len(batches) == 2
+    obs_b, hxs_b, act_b, vp_b, ret_b, m_b, lp_b, adv_b = batches[0]
+    ind = perm[:2]
+    assert obs_b["spatial_edges"].shape == (T * 2, N, 2)
+    assert hxs_b["human_human_edge_rnn"].shape == (2, N + 1, 256)
+    np.testing.assert_array_equal(adv_b.numpy().reshape(T, 2), adv[:, ind, 0].numpy())
+    np.testing.assert_array_equal(hxs_b["human_node_rnn"].numpy(), rol.recurrent_hidden_states["human_node_rnn"][0, ind].numpy())
+    np.testing.assert_array_equal(obs_b["robot_node"].numpy().reshape(T, 2, 1, 7), rol.obs["robot_node"][:-1, ind].numpy())
+
+
+def test_compact_hidden_same_minibatches(fx):
+    """compact_hidden keeps slots {start, latest}: the generator and after_update see the same states."""
+    full, comp = _filled(fx), _filled(fx, compact=True)
+    assert comp.recurrent_hidden_states["human_human_edge_rnn"].shape[0] == 2
+    for t in (0, 3, T):
+        want = {k: v[t] for k, v in full.recurrent_hidden_states.items()} if t in (0, T) else None
+        if want is not None:
+            got = comp.hidden(t)
+            for k in want:
+                assert torch.equal(got[k], want[k])
+    adv = torch.randn(T, E, 1)
+    torch.manual_seed(3)
+    a = list(full.recurrent_generator(adv, 2))
+    torch.manual_seed(3)
+    b = list(comp.recurrent_generator(adv, 2))
+    for x, y in zip(a, b):
+        for k in x[1]:
+            assert torch.equal(x[1][k], y[1][k])
+    full.after_update()
+    comp.after_update()
+    for k in full.recurrent_hidden_states:
+        assert torch.equal(full.recurrent_hidden_states[k][0], comp.recurrent_hidden_states[k][0])
+
+
+def _update(fx, device):
+    pol = make_policy(N, E=E, T=T, device=device)
+    pol.base.nminibatch = 2
+    pol.train()
+    rol = _filled(fx, device)
+    rol.compute_returns(torch.from_numpy(fx["next_value"]).to(device), True, 0.99, 0.95, True)
+    agent = PPO(pol, 0.2, 2, 2, 0.5, 0.01, lr=4e-5, eps=1e-5, max_grad_norm=0.5)
+    torch.manual_seed(1234)
+    losses = agent.update(rol)
+    return pol, losses
+
+
+def test_ppo_update_cpu(fx, monkeypatch):
+    """The whole update on CPU (the fused input-layer kernel replaced by its fp32 torch restatement)."""
+    from crowdnav_dsrnn_amd import ops
+
+    monkeypatch.setattr(ops, "edge_features", edge_features_fp32)
+    pol, losses = _update(fx, "cpu")
+    np.testing.assert_allclose(losses, fx["update_losses"], atol=2e-6, rtol=1e-5)
+    for k, v in pol.state_dict().items():
+        np.testing.assert_allclose(v.numpy(), fx["param_" + k], atol=1e-6, rtol=0, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_ppo_update_gpu(fx):
+    pol, losses = _update(fx, "cuda:0")
+    np.testing.assert_allclose(losses, fx["update_losses"], atol=5e-5, rtol=1e-4)
+    for k, v in pol.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), fx["param_" + k], atol=5e-6, rtol=0, err_msg=k)
+
+
+def _dist_worker(rank, world, port, out):
+    import torch.distributed as dist
+
+    from crowdnav_dsrnn_amd import ops
+
+    ops.edge_features = edge_features_fp32
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fx = load("ppo.npz")
+        torch.manual_seed(100 + rank)          # different initial weights per rank: PPO broadcasts rank 0's
+        pol = make_policy(N, E=E, T=T)
+        if rank == 1:
+            for p in pol.parameters():
+                p.data.add_(0.01)
+        pol.base.nminibatch = 2
+        pol.train()
+        rol = _filled(fx)
+        if rank == 1:                          # each rank holds different rollouts
+            rol.rewards.mul_(-0.5)
+        rol.compute_returns(torch.from_numpy(fx["next_value"]), True, 0.99, 0.95, True)
+        agent = PPO(pol, 0.2, 1, 2, 0.5, 0.01, lr=4e-5, eps=1e-5, max_grad_norm=0.5)
+        adv = agent._normalised_advantages(rol)
+        torch.manual_seed(1234)
+        agent.update(rol)
+        flat = torch.cat([p.detach().reshape(-1) for p in pol.parameters()])
+        raw = (rol.returns[:-1] - rol.value_preds[:-1]).reshape(-1)
+        torch.save({"flat": flat, "adv": adv.reshape(-1), "raw": raw}, "%s.%d" % (out, rank))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ppo_data_parallel_gloo(tmp_path):
+    """world_size 2: ranks start identical (broadcast), stay identical after the all-reduced update, and
+    normalise advantages with the global mean / unbiased std."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "r")
+    mp.start_processes(_dist_worker, args=(2, port, out), nprocs=2, join=True, start_method="spawn")
+    r0, r1 = torch.load(out + ".0", weights_only=True), torch.load(out + ".1", weights_only=True)
+    assert torch.equal(r0["flat"], r1["flat"])
+    raw = torch.cat([r0["raw"], r1["raw"]]).double()
+    mean, std = raw.mean(), raw.std()
+    np.testing.assert_allclose(r0["adv"].numpy(), ((r0["raw"].double() - mean) / (std + 1e-5)).numpy(), atol=1e-5)
+    np.testing.assert_allclose(r1["adv"].numpy(), ((r1["raw"].double() - mean) / (std + 1e-5)).numpy(), atol=1e-5)
