@@ -7,7 +7,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libcrowdnav_hip.so")
-SOURCES = [os.path.join(HERE, "csrc", "cn_engine.hip")]
+SOURCES = [os.path.join(HERE, "csrc", "cn_engine.hip"), os.path.join(HERE, "csrc", "cn_gru.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "cn_math.h"), os.path.join(REPO, "include", "crowdnav.h"),
                   os.path.join(REPO, "include", "crowdnav_state.h")]
 ARCH = os.environ.get("CN_OFFLOAD_ARCH", "gfx950")

@@ -2278,6 +2278,7 @@ static int set_err(int code, const char *fmt, const char *a = "")
     snprintf(g_err, sizeof g_err, fmt, a);
     return code;
 }
+int cn_set_error(int code, const char *msg) { return set_err(code, "%s", msg); }   // for cn_gru.hip
 #define HIPCHK(x)                                                                       \
     do {                                                                                \
         hipError_t _e = (x);                                                            \

@@ -1,0 +1,149 @@
+// Masked GRU sequence kernels for the DSRNN policy.
+//
+// The reference runs its three GRUs (srnn_model.py:52-104, RNNBase._forward_gru) as torch nn.GRU calls over
+// the segments between episode starts; every segment boundary re-enters cuDNN/MIOpen with the hidden state
+// multiplied by the mask. Here a sequence of T steps is:
+//   gi  = x @ W_ih^T + b_ih            one GEMM over all T*B rows (hipBLASLt, from the torch wrapper)
+//   per step t:
+//     gh = hm_t @ W_hh^T + b_hh        one GEMM (B x H -> B x 3H)
+//     cn_gru_fwd_step                  gates + new state + the next step's masked state, one pass
+//   backward, per step t (reversed):
+//     cn_gru_bwd_step                  gate gradients from the saved gates, one pass
+//     acc += dgh_t @ W_hh              one GEMM
+//   then dW_ih, dW_hh, db_*, dx as single GEMMs / reductions over all T*B rows.
+// Gate math and operation order follow ATen's GRU cell (the reference's nn.GRU):
+//   r = sigmoid(gh_r + gi_r), z = sigmoid(gh_z + gi_z), n = tanh(gi_n + r * gh_n), h' = (h - n) * z + n.
+// Memory-bound elementwise work: each thread handles 4 consecutive hidden units (16-byte accesses).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/crowdnav.h"
+
+int cn_set_error(int code, const char *msg);
+
+namespace {
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// gi, gh: [B][3H] (r | z | n blocks); hm: [B][H] the masked previous state; m_next: [B] or null;
+// h_out: [B][H]; hm_next: [B][H] or null (= h_out * m_next); save: [B][4H] (r | z | n | gh_n) or null.
+__global__ __launch_bounds__(256) void cn_gru_fwd_kernel(int64_t B, int H, const float *__restrict__ gi,
+                                                         const float *__restrict__ gh,
+                                                         const float *__restrict__ hm,
+                                                         const float *__restrict__ m_next, float *__restrict__ h_out,
+                                                         float *__restrict__ hm_next, float *__restrict__ save)
+{
+    const int H4 = H >> 2;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * H4) return;
+    const int64_t b = i / H4;
+    const int j = (int)(i - b * H4) * 4;
+    const float4 ir = *(const float4 *)(gi + b * 3 * H + j);
+    const float4 iz = *(const float4 *)(gi + b * 3 * H + H + j);
+    const float4 in = *(const float4 *)(gi + b * 3 * H + 2 * H + j);
+    const float4 hr = *(const float4 *)(gh + b * 3 * H + j);
+    const float4 hz = *(const float4 *)(gh + b * 3 * H + H + j);
+    const float4 hn = *(const float4 *)(gh + b * 3 * H + 2 * H + j);
+    const float4 hp = *(const float4 *)(hm + b * H + j);
+    float4 r, z, n, h;
+#define CN_GATE(c)                                 \
+    r.c = sigm(hr.c + ir.c);                       \
+    z.c = sigm(hz.c + iz.c);                       \
+    n.c = tanhf(in.c + hn.c * r.c);                \
+    h.c = (hp.c - n.c) * z.c + n.c;
+    CN_GATE(x) CN_GATE(y) CN_GATE(z) CN_GATE(w)
+#undef CN_GATE
+    *(float4 *)(h_out + b * H + j) = h;
+    if (hm_next) {
+        const float m = m_next ? m_next[b] : 1.0f;
+        *(float4 *)(hm_next + b * H + j) = make_float4(h.x * m, h.y * m, h.z * m, h.w * m);
+    }
+    if (save) {
+        float *s = save + b * 4 * H + j;
+        *(float4 *)(s) = r;
+        *(float4 *)(s + H) = z;
+        *(float4 *)(s + 2 * H) = n;
+        *(float4 *)(s + 3 * H) = hn;
+    }
+}
+
+// Gradient of step t. g = acc * m_next + dout_t is dL/dh_t (acc = dL/dhm_{t+1} from the later step, or
+// dL/dh_T at the last step with m_next = null). Writes dgi_t, dgh_t [B][3H] and acc <- g * z (the direct
+// path of dL/dhm_t; the caller adds dgh_t @ W_hh).
+__global__ __launch_bounds__(256) void cn_gru_bwd_kernel(int64_t B, int H, float *__restrict__ acc,
+                                                         const float *__restrict__ m_next,
+                                                         const float *__restrict__ dout,
+                                                         const float *__restrict__ save,
+                                                         const float *__restrict__ hm, float *__restrict__ dgi,
+                                                         float *__restrict__ dgh)
+{
+    const int H4 = H >> 2;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B * H4) return;
+    const int64_t b = i / H4;
+    const int j = (int)(i - b * H4) * 4;
+    const float m = m_next ? m_next[b] : 1.0f;
+    float4 g = *(const float4 *)(acc + b * H + j);
+    g = make_float4(g.x * m, g.y * m, g.z * m, g.w * m);
+    if (dout) {
+        const float4 d = *(const float4 *)(dout + b * H + j);
+        g = make_float4(g.x + d.x, g.y + d.y, g.z + d.z, g.w + d.w);
+    }
+    const float *s = save + b * 4 * H + j;
+    const float4 r = *(const float4 *)(s), z = *(const float4 *)(s + H), n = *(const float4 *)(s + 2 * H),
+                 hn = *(const float4 *)(s + 3 * H);
+    const float4 hp = *(const float4 *)(hm + b * H + j);
+    float4 a, dr, dz, dn, dhn;
+#define CN_GBWD(c)                                              \
+    {                                                           \
+        const float dnc = g.c * (1.0f - z.c) * (1.0f - n.c * n.c); \
+        const float dzc = g.c * (hp.c - n.c) * z.c * (1.0f - z.c); \
+        const float drc = dnc * hn.c * r.c * (1.0f - r.c);      \
+        a.c = g.c * z.c;                                        \
+        dr.c = drc;                                             \
+        dz.c = dzc;                                             \
+        dn.c = dnc;                                             \
+        dhn.c = dnc * r.c;                                      \
+    }
+    CN_GBWD(x) CN_GBWD(y) CN_GBWD(z) CN_GBWD(w)
+#undef CN_GBWD
+    *(float4 *)(acc + b * H + j) = a;
+    *(float4 *)(dgi + b * 3 * H + j) = dr;
+    *(float4 *)(dgi + b * 3 * H + H + j) = dz;
+    *(float4 *)(dgi + b * 3 * H + 2 * H + j) = dn;
+    *(float4 *)(dgh + b * 3 * H + j) = dr;
+    *(float4 *)(dgh + b * 3 * H + H + j) = dz;
+    *(float4 *)(dgh + b * 3 * H + 2 * H + j) = dhn;
+}
+
+inline unsigned grid_for(int64_t B, int H) { return (unsigned)((B * (H / 4) + 255) / 256); }
+
+}  // namespace
+
+extern "C" {
+
+int cn_gru_fwd_step(void *stream, int64_t B, int H, const float *gi, const float *gh, const float *hm,
+                    const float *m_next, float *h_out, float *hm_next, float *save)
+{
+    if (B <= 0 || H <= 0 || (H & 3)) return cn_set_error(CN_EINVAL, "cn_gru_fwd_step: B > 0 and H % 4 == 0 required");
+    if (!gi || !gh || !hm || !h_out) return cn_set_error(CN_EINVAL, "cn_gru_fwd_step: null operand");
+    if (B * (H / 4) > (int64_t)0xffffffff * 256) return cn_set_error(CN_EINVAL, "cn_gru_fwd_step: B too large");
+    hipLaunchKernelGGL(cn_gru_fwd_kernel, dim3(grid_for(B, H)), dim3(256), 0, (hipStream_t)stream, B, H, gi, gh,
+                       hm, m_next, h_out, hm_next, save);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
+                    const float *save, const float *hm, float *dgi, float *dgh)
+{
+    if (B <= 0 || H <= 0 || (H & 3)) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step: B > 0 and H % 4 == 0 required");
+    if (!acc || !save || !hm || !dgi || !dgh) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step: null operand");
+    if (B * (H / 4) > (int64_t)0xffffffff * 256) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step: B too large");
+    hipLaunchKernelGGL(cn_gru_bwd_kernel, dim3(grid_for(B, H)), dim3(256), 0, (hipStream_t)stream, B, H, acc,
+                       m_next, dout, save, hm, dgi, dgh);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+}  // extern "C"

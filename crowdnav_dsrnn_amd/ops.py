@@ -3,6 +3,8 @@
 edge_features(...)  — the fused DSRNN input layers (cn_edge_features, include/crowdnav.h): one launch
                       computes relu(temporal encoder), relu(spatial encoder) and
                       relu(node encoder(robot_linear(robot_node))) for every env (and time step).
+masked_gru(...)     — the mask-segmented GRU of the three DSRNN RNNs over a (T, B) sequence
+                      (cn_gru_fwd_step / cn_gru_bwd_step + library GEMMs), with its own backward.
 """
 import torch
 
@@ -70,3 +72,79 @@ def edge_features(robot_node, temporal, spatial, Wt, bt, Ws, bs, Wr, br, Wn, bn)
         raise EdgeFeaturesUnavailable("the DSRNN edge-feature layers run only as the fused HIP kernel "
                                       "(tensors are on %s)" % robot_node.device)
     return _EdgeFeatures.apply(robot_node, temporal, spatial, Wt, bt, Ws, bs, Wr, br, Wn, bn)
+
+
+class _MaskedGRU(torch.autograd.Function):
+    """srnn_model.py:52-104 (RNNBase._forward_gru): h <- h * mask[t] before step t, then one nn.GRU step.
+
+    Forward: gi = x W_ih^T + b_ih as one GEMM over all T*B rows; per step one GEMM gh = hm W_hh^T + b_hh
+    and one cn_gru_fwd_step (gates, new state, next masked state; saves r|z|n|gh_n when a gradient is
+    needed). Backward: per step (reversed) one cn_gru_bwd_step and one GEMM acc += dgh W_hh, then the
+    weight / input gradients as single GEMMs over all T*B rows."""
+
+    @staticmethod
+    def forward(ctx, x, h0, masks, w_ih, w_hh, b_ih, b_hh):
+        T, B, F = x.shape
+        H = w_hh.shape[1]
+        dev = x.device
+        need = any(ctx.needs_input_grad)
+        L = _lib.lib()
+        st = _stream(dev)
+        x2 = _c(x).reshape(T * B, F)
+        m = _c(masks).reshape(T, B)
+        gi = torch.addmm(b_ih, x2, w_ih.t()).reshape(T, B, 3 * H)
+        out = torch.empty((T, B, H), dtype=torch.float32, device=dev)
+        if need:
+            hm = torch.empty((T, B, H), dtype=torch.float32, device=dev)
+            save = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
+        else:
+            hm = torch.empty((min(T, 2), B, H), dtype=torch.float32, device=dev)
+            save = None
+        torch.mul(h0, m[0].unsqueeze(-1), out=hm[0])
+        gh = torch.empty((B, 3 * H), dtype=torch.float32, device=dev)
+        nh = hm.shape[0]
+        with torch.cuda.device(dev):
+            for t in range(T):
+                cur = hm[t % nh]
+                torch.addmm(b_hh, cur, w_hh.t(), out=gh)
+                last = t + 1 == T
+                _lib.check(L.cn_gru_fwd_step(st, B, H, gi[t].data_ptr(), gh.data_ptr(), cur.data_ptr(),
+                                             None if last else m[t + 1].data_ptr(), out[t].data_ptr(),
+                                             None if last else hm[(t + 1) % nh].data_ptr(),
+                                             save[t].data_ptr() if need else None))
+        if need:
+            ctx.save_for_backward(x2, m, w_ih, w_hh, hm, save)
+        return out, out[-1].clone()
+
+    @staticmethod
+    def backward(ctx, dout, dhT):
+        x2, m, w_ih, w_hh, hm, save = ctx.saved_tensors
+        T, B, H = hm.shape
+        dev = x2.device
+        L = _lib.lib()
+        st = _stream(dev)
+        acc = dhT.contiguous().clone() if dhT is not None else torch.zeros((B, H), dtype=torch.float32, device=dev)
+        dout = dout.contiguous() if dout is not None else None
+        dgi = torch.empty((T, B, 3 * H), dtype=torch.float32, device=dev)
+        dgh = torch.empty((T, B, 3 * H), dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            for t in reversed(range(T)):
+                _lib.check(L.cn_gru_bwd_step(st, B, H, acc.data_ptr(), None if t + 1 == T else m[t + 1].data_ptr(),
+                                             dout[t].data_ptr() if dout is not None else None, save[t].data_ptr(),
+                                             hm[t].data_ptr(), dgi[t].data_ptr(), dgh[t].data_ptr()))
+                acc.addmm_(dgh[t], w_hh)
+        dh0 = acc * m[0].unsqueeze(-1)
+        dgi2 = dgi.reshape(T * B, 3 * H)
+        dgh2 = dgh.reshape(T * B, 3 * H)
+        dx = (dgi2 @ w_ih).reshape(T, B, -1) if ctx.needs_input_grad[0] else None
+        return (dx, dh0, None, dgi2.t() @ x2, dgh2.t() @ hm.reshape(T * B, H), dgi2.sum(0), dgh2.sum(0))
+
+
+def masked_gru(x, h0, masks, w_ih, w_hh, b_ih, b_hh):
+    """x (T,B,F), h0 (B,H), masks (T,B) -> out (T,B,H), h_T (B,H); the weights of a 1-layer nn.GRU."""
+    if not x.is_cuda:
+        raise EdgeFeaturesUnavailable("the DSRNN GRUs run only through the HIP step kernels (cn_gru_*); "
+                                      "tensors are on %s" % x.device)
+    if x.dtype != torch.float32 or w_hh.shape[1] % 4:
+        raise ValueError("masked_gru: fp32 operands and a hidden size divisible by 4 required")
+    return _MaskedGRU.apply(x, h0, masks, w_ih, w_hh, b_ih, b_hh)

@@ -39,18 +39,10 @@ class RNNBase(nn.Module):
 
     def masked_gru(self, x, h0, masks):
         """x (T, B, F), h0 (B, H), masks (T, B) -> out (T, B, H), h_T (B, H).
-        h <- h * mask[t] before step t (episode starts), then one GRU step."""
-        T = x.shape[0]
-        if T == 1:
-            out, h = self.gru(x, (h0 * masks[0].unsqueeze(-1)).unsqueeze(0))
-            return out, h[0]
-        outs = []
-        h = h0
-        for t in range(T):
-            o, hn = self.gru(x[t:t + 1], (h * masks[t].unsqueeze(-1)).unsqueeze(0))
-            outs.append(o)
-            h = hn[0]
-        return torch.cat(outs, 0), h
+        h <- h * mask[t] before step t (episode starts), then one GRU step (srnn_model.py:52-104);
+        runs as ops.masked_gru (HIP gate kernels + GEMMs)."""
+        g = self.gru
+        return ops.masked_gru(x, h0, masks, g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0)
 
 
 class HumanNodeRNN(RNNBase):

@@ -19,6 +19,9 @@
  *                   HumanHumanEdgeRNN.encoder_linear+ReLU (srnn_model.py:210-211) for the temporal and
  *                   spatial edges, SRNN.robot_linear (srnn_model.py:466) and
  *                   HumanNodeRNN.encoder_linear+ReLU (srnn_model.py:160-161)
+ *   cn_gru_fwd_step / cn_gru_bwd_step ⟵ one time step of the mask-segmented GRU
+ *                   (srnn_model.py:52-104 RNNBase._forward_gru, torch nn.GRU cell math) and its gradient;
+ *                   the GEMMs around them (x W_ih^T, hm W_hh^T, dgh W_hh) are library GEMMs
  *
  * Conventions
  *   - All array arguments are DEVICE pointers (torch tensors' data_ptr()), row-major, caller-owned.
@@ -177,6 +180,21 @@ int cn_edge_features(void *stream, int64_t E, int N,
                      const float *Wt, const float *bt, const float *Ws, const float *bs,
                      const float *Wr, const float *br, const float *Wn, const float *bn,
                      float *temporal_embed, float *spatial_embed, float *node_embed);
+
+/* One GRU step after the two GEMMs (nn.GRU gate order r | z | n, ATen's cell arithmetic):
+ *   r = sigmoid(gh_r + gi_r), z = sigmoid(gh_z + gi_z), n = tanh(gi_n + r * gh_n), h = (hm - n) * z + n
+ * gi = x W_ih^T + b_ih, gh = hm W_hh^T + b_hh: [B][3H]; hm: [B][H] (previous state times this step's mask);
+ * m_next [B] (next step's mask; NULL = 1); out h_out [B][H]; hm_next [B][H] = h * m_next (NULL = skip);
+ * save [B][4H] = r | z | n | gh_n for the backward (NULL = skip). H % 4 == 0. */
+int cn_gru_fwd_step(void *stream, int64_t B, int H, const float *gi, const float *gh, const float *hm,
+                    const float *m_next, float *h_out, float *hm_next, float *save);
+
+/* Gradient of one step. In: acc [B][H] = dL/dhm of the later step (or dL/dh_T at the last step, with
+ * m_next = NULL), m_next [B] that later step's mask, dout [B][H] = dL/dh_t from the outputs (NULL = 0),
+ * save / hm as written by the forward. Out: dgi, dgh [B][3H] (pre-activation gradients of gi, gh) and
+ * acc <- dL/dh_t * z (the caller then adds dgh W_hh to obtain dL/dhm_t). */
+int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
+                    const float *save, const float *hm, float *dgi, float *dgh);
 
 #ifdef __cplusplus
 }

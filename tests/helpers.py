@@ -208,3 +208,16 @@ def edge_features_fp32(robot_node, temporal, spatial, Wt, bt, Ws, bs, Wr, br, Wn
     s = torch.relu(spatial.reshape(E * N, 2) @ Ws.t() + bs).reshape(E, N, 64)
     n = torch.relu((robot_node.reshape(E, 7) @ Wr.t() + br) @ Wn.t() + bn)
     return t, s, n
+
+
+def masked_gru_ref(x, h0, masks, w_ih, w_hh, b_ih, b_hh):
+    """Plain PyTorch fp32 restatement of the mask-segmented GRU (srnn_model.py:52-104): per step
+    h <- h * mask[t], then torch.gru_cell (nn.GRU's cell)."""
+    import torch
+
+    outs = []
+    h = h0
+    for t in range(x.shape[0]):
+        h = torch.gru_cell(x[t], h * masks[t].unsqueeze(-1), w_ih, w_hh, b_ih, b_hh)
+        outs.append(h)
+    return torch.stack(outs, 0), h

@@ -11,7 +11,7 @@ import torch
 
 from crowdnav_dsrnn_amd.learner import PPO, SRNNRolloutStorage
 from crowdnav_dsrnn_amd.spaces import Box
-from tests.helpers import edge_features_fp32, load, make_policy
+from tests.helpers import edge_features_fp32, masked_gru_ref, load, make_policy
 
 N, E, T = 5, 4, 8
 
@@ -107,6 +107,7 @@ def test_ppo_update_cpu(fx, monkeypatch):
     from crowdnav_dsrnn_amd import ops
 
     monkeypatch.setattr(ops, "edge_features", edge_features_fp32)
+    monkeypatch.setattr(ops, "masked_gru", masked_gru_ref)
     pol, losses = _update(fx, "cpu")
     np.testing.assert_allclose(losses, fx["update_losses"], atol=2e-6, rtol=1e-5)
     for k, v in pol.state_dict().items():
@@ -127,6 +128,7 @@ def _dist_worker(rank, world, port, out):
     from crowdnav_dsrnn_amd import ops
 
     ops.edge_features = edge_features_fp32
+    ops.masked_gru = masked_gru_ref
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests.helpers import edge_features_fp32, load, make_policy
+from tests.helpers import edge_features_fp32, masked_gru_ref, load, make_policy
 
 ATOL, RTOL = 2e-5, 1e-4
 
@@ -88,6 +88,7 @@ def test_policy_graph_cpu_with_fp32_input_layers(dsrnn, N, monkeypatch):
     from crowdnav_dsrnn_amd import ops
 
     monkeypatch.setattr(ops, "edge_features", edge_features_fp32)
+    monkeypatch.setattr(ops, "masked_gru", masked_gru_ref)
     _check_act(dsrnn, N, _run_act(dsrnn, N, "cpu"))
     _check_eval(dsrnn, N, _run_eval(dsrnn, N, "cpu"))
 
@@ -136,3 +137,37 @@ def test_edge_features_backward_vs_fp32():
     sum((o * wi.to("cuda:0")).sum() for o, wi in zip(ops.edge_features(*a_gpu), w)).backward()
     for x, y in zip(a_cpu, a_gpu):
         np.testing.assert_allclose(y.grad.cpu().numpy(), x.grad.numpy(), atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,B,F,H", [(1, 45, 64, 256), (9, 33, 64, 256), (16, 70, 128, 128)])
+def test_masked_gru_kernels_vs_fp64(T, B, F, H):
+    """cn_gru_fwd_step / cn_gru_bwd_step (+ GEMMs) vs the plain torch restatement of the mask-segmented GRU
+    (srnn_model.py:52-104) in float64: outputs, final state and every input / weight gradient, with episode
+    starts at step 0 and mid-sequence. fp32 GEMM/transcendental rounding: atol 2e-5 (outputs), 1e-4 x scale
+    (gradients)."""
+    from crowdnav_dsrnn_amd import ops
+
+    g = torch.Generator().manual_seed(T * 1000 + B)
+    x = torch.randn(T, B, F, generator=g)
+    h0 = torch.randn(B, H, generator=g) * 0.5
+    masks = (torch.rand(T, B, generator=g) > 0.2).float()
+    masks[:, 0] = 0.0
+    gru = torch.nn.GRU(F, H)
+    ws = [gru.weight_ih_l0.detach(), gru.weight_hh_l0.detach(),
+          torch.randn(3 * H, generator=g) * 0.1, torch.randn(3 * H, generator=g) * 0.1]
+    dout = torch.randn(T, B, H, generator=g)
+    dhT = torch.randn(B, H, generator=g)
+
+    def run(fn, dev, dt):
+        leaves = [t.to(dev, dt).requires_grad_(True) for t in (x, h0, *ws)]
+        out, hT = fn(leaves[0], leaves[1], masks.to(dev, dt), *leaves[2:])
+        ((out * dout.to(dev, dt)).sum() + (hT * dhT.to(dev, dt)).sum()).backward()
+        return [out.detach().cpu().double(), hT.detach().cpu().double()] + [l.grad.cpu().double() for l in leaves]
+
+    got = run(ops.masked_gru, "cuda:0", torch.float32)
+    want = run(masked_gru_ref, "cpu", torch.float64)
+    names = ["out", "hT", "dx", "dh0", "dW_ih", "dW_hh", "db_ih", "db_hh"]
+    for n, a, b in zip(names, got, want):
+        tol = 2e-5 if n in ("out", "hT") else 1e-4 * max(1.0, float(b.abs().max()))
+        np.testing.assert_allclose(a.numpy(), b.numpy(), atol=tol, rtol=0, err_msg=n)
