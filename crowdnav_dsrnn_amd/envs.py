@@ -174,7 +174,7 @@ class CrowdNavVecEnv:
     """E CrowdSimDict envs on one GPU with VecPyTorch/ShmemVecEnv/Monitor semantics."""
 
     def __init__(self, config, num_envs, seed, device, allow_early_resets=False, env_offset=0, nenv=None,
-                 engine_device=None):
+                 engine_device=None, phase=None):
         import torch
 
         from .engine import CrowdNavEngine
@@ -183,8 +183,9 @@ class CrowdNavVecEnv:
         self.config = config
         self.num_envs = int(num_envs)
         nenv = self.num_envs if nenv is None else int(nenv)
-        self.phase = "train" if nenv > 1 else "test"
+        self.phase = phase if phase is not None else ("train" if nenv > 1 else "test")
         self.cn_cfg = make_cn_config(config, num_envs=self.num_envs, env_offset=env_offset, nenv=nenv,
+                                     phase=self.phase,
                                      seed=seed if seed is not None else config.env.seed)
         self.device = torch.device(device)
         if engine_device is None and self.device.type == "cuda":

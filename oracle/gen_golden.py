@@ -12,6 +12,8 @@ oracle/shims (gym, shapely, rvo2, torchvision — see oracle/shims/README.md) an
                  (shmem_vec_env.py:164-168) and bench.Monitor's episode return
   dsrnn.npz      DSRNN Policy.act / evaluate_actions with procedural weights
                  (pytorchBaselines/a2c_ppo_acktr/model.py:63-104, srnn_model.py:409-504)
+  eval_*.npz     pytorchBaselines/evaluation.py evaluate() + metrics.py Metrics driven by a scripted
+                 episode stream (stand-in VecEnv / policy objects; the bookkeeping is the reference's)
   ppo.npz        SRNNRolloutStorage + compute_returns + PPO.update on procedural weights
                  (pytorchBaselines/a2c_ppo_acktr/storage.py:14-292, algo/ppo.py:36-118)
 
@@ -527,6 +529,169 @@ def gen_ppo(outdir):
     print("ppo ok")
 
 
+EVAL_SCEN = ("circle_crossing", "square_crossing", "parallel_traffic")
+
+
+def make_eval_script(n_ep, seed, scenarios, side_scenario=None, max_len=25):
+    """A synthetic test-episode stream in the VecEnv's step format (float32 obs / reward / info values):
+    per episode a spawn (reset obs, zero velocity) and per step the post-step robot position / velocity,
+    reward, event code, info fields. Terminal events cycle through success / collision / timeout."""
+    rng = np.random.RandomState(seed)
+    f32 = lambda x: float(np.float32(x))  # noqa: E731
+    eps = []
+    for k in range(n_ep):
+        L = int(rng.randint(1, max_len + 1))
+        first = rng.uniform(-6, 6, 2).astype(np.float32)
+        term = [abi.EV_REACHGOAL, abi.EV_COLLISION, abi.EV_TIMEOUT][int(rng.randint(3)) if k > 2 else k]
+        scen = scenarios[int(rng.randint(len(scenarios)))] if side_scenario is None else side_scenario
+        pos = first.copy()
+        steps = []
+        for t in range(L):
+            pos = (pos + rng.uniform(-0.3, 0.3, 2)).astype(np.float32)
+            vel = rng.uniform(-1, 1, 2).astype(np.float32)
+            ev = term if t == L - 1 else (abi.EV_DANGER if rng.rand() < 0.25 else abi.EV_NOTHING)
+            st = {"pos": pos.copy(), "vel": vel, "reward": f32(rng.normal()), "event": ev,
+                  "min_dist": f32(rng.uniform(0, 0.25)),
+                  "aggregate_nav_time": int(rng.randint(0, 3)), "path_violation": int(rng.randint(0, 3)),
+                  "personal_violation": int(rng.rand() < 0.3), "jerk_cost": f32(rng.uniform(0, 2)) * (rng.rand() < 0.7),
+                  "dist_to_goal": f32(rng.uniform(0, 9)) * (rng.rand() < 0.9),
+                  "speed_violation": int(rng.rand() < 0.2), "left": int(rng.rand() < 0.4),
+                  "right": int(rng.rand() < 0.4)}
+            steps.append(st)
+        eps.append({"first": first, "scenario": scen, "steps": steps})
+    return eps
+
+
+def run_ref_evaluate(cfg, eps):
+    """Drive pytorchBaselines/evaluation.py:evaluate (1 env, sequential episodes) over the script with
+    stand-in env / policy objects; returns (log lines, raw_rewards, discounted_rewards, dist_to_goal)."""
+    import contextlib
+    import io
+
+    import torch
+    from crowd_sim.envs.utils import info as ref_info
+    from pytorchBaselines.evaluation import evaluate as ref_evaluate
+
+    dt = cfg.env.time_step
+    side = cfg.test.side_preference
+    ev_cls = {abi.EV_NOTHING: lambda d: ref_info.Nothing(), abi.EV_DANGER: lambda d: ref_info.Danger(d),
+              abi.EV_COLLISION: lambda d: ref_info.Collision(), abi.EV_REACHGOAL: lambda d: ref_info.ReachGoal(),
+              abi.EV_TIMEOUT: lambda d: ref_info.Timeout()}
+
+    def obs_of(pos, vel):
+        rn = torch.zeros(1, 1, 7)
+        rn[0, 0, 0], rn[0, 0, 1] = float(pos[0]), float(pos[1])
+        te = torch.tensor([[[float(vel[0]), float(vel[1])]]], dtype=torch.float32)
+        return {"robot_node": rn, "temporal_edges": te, "spatial_edges": torch.zeros(1, 1, 2)}
+
+    class Robot:
+        time_step = dt
+        v_pref = cfg.robot.v_pref
+
+    class BaseEnv:
+        time_step = dt
+        time_limit = cfg.env.time_limit
+        robot = Robot()
+        global_time = 0.0
+
+    class Envs:
+        def __init__(self):
+            self.base = BaseEnv()
+            self.venv = type("V", (), {})()
+            self.venv.envs = [type("M", (), {"env": self.base})()]
+            self.k, self.t = 0, 0
+
+        def reset(self):
+            e = eps[0]
+            return obs_of(e["first"], (0.0, 0.0))
+
+        def step(self, action):
+            e = eps[self.k % len(eps)]
+            st = e["steps"][self.t]
+            self.t += 1
+            done = self.t == len(e["steps"])
+            si = {"aggregate_nav_time": st["aggregate_nav_time"], "path_violation": st["path_violation"]}
+            if side:
+                si[e["scenario"]] = {"left": st["left"], "right": st["right"]}
+            si.update(personal_violation=st["personal_violation"], jerk_cost=st["jerk_cost"],
+                      dist_to_goal=st["dist_to_goal"], speed_violation=st["speed_violation"],
+                      scenario=e["scenario"], event=ev_cls[st["event"]](st["min_dist"]))
+            self.base.global_time += dt
+            if done:
+                self.k += 1
+                self.t = 0
+                self.base.global_time = 0.0
+                nxt = eps[self.k % len(eps)]
+                ob = obs_of(nxt["first"], (0.0, 0.0))
+            else:
+                ob = obs_of(st["pos"], st["vel"])
+            return ob, torch.tensor([[st["reward"]]], dtype=torch.float32), np.array([done]), ({"info": si},)
+
+        def close(self):
+            pass
+
+    class Pol:
+        base = type("B", (), {"human_num": 1})()
+
+        def act(self, obs, hxs, masks, deterministic=False):
+            return None, torch.zeros(1, 2), None, hxs
+
+    class Log:
+        lines = []
+
+        def info(self, msg):
+            self.lines.append(str(msg))
+
+    log = Log()
+    log.lines = []
+    with contextlib.redirect_stdout(io.StringIO()):
+        raw, disc, d2g = ref_evaluate(Pol(), False, Envs(), 1, "cpu", cfg, log)
+    return log.lines, raw, disc, d2g
+
+
+def pack_eval_script(eps, out):
+    names = sorted(set(e["scenario"] for e in eps))
+    out["ep_len"] = np.array([len(e["steps"]) for e in eps], np.int32)
+    out["ep_first"] = np.stack([e["first"] for e in eps]).astype(np.float32)
+    out["ep_scenario"] = np.array([e["scenario"] for e in eps])
+    cat = lambda key, dt: np.array([st[key] for e in eps for st in e["steps"]], dt)  # noqa: E731
+    out["st_pos"] = np.stack([st["pos"] for e in eps for st in e["steps"]]).astype(np.float32)
+    out["st_vel"] = np.stack([st["vel"] for e in eps for st in e["steps"]]).astype(np.float32)
+    for key, dt in (("reward", np.float32), ("event", np.int8), ("min_dist", np.float32),
+                    ("aggregate_nav_time", np.int32), ("path_violation", np.int32),
+                    ("personal_violation", np.int32), ("jerk_cost", np.float32), ("dist_to_goal", np.float32),
+                    ("speed_violation", np.int32), ("left", np.int32), ("right", np.int32)):
+        out["st_" + key] = cat(key, dt)
+    return names
+
+
+def gen_eval(outdir):
+    """evaluate() golden logs / returns for two configurations (social metrics; side preference)."""
+    cases = [("eval_social", dict(scenarios=EVAL_SCEN, social_metrics=True), 16, None),
+             ("eval_sidepref", dict(scenarios=("side_pref_passing",), side_pref=True, N=1), 12, "side_pref_passing")]
+    for name, kw, n_ep, side_scen in cases:
+        cfg = make_ref_config(**kw)
+        cfg.env.test_size = n_ep
+        eps = make_eval_script(n_ep, 7 + n_ep, list(kw["scenarios"]), side_scen)
+        lines, raw, disc, d2g = run_ref_evaluate(cfg, eps)
+        out = {}
+        pack_eval_script(eps, out)
+        out["log"] = np.array("\n".join(lines))
+        out["test_size"] = np.int32(n_ep)
+        out["time_step"] = np.float64(cfg.env.time_step)
+        out["time_limit"] = np.float64(cfg.env.time_limit)
+        out["social_metrics"] = np.int32(cfg.test.social_metrics)
+        out["side_preference"] = np.int32(cfg.test.side_preference)
+        out["train_val_sim"] = np.array(cfg.sim.train_val_sim)
+        out["test_sim"] = np.array(cfg.sim.test_sim)
+        for tag, d in (("raw", raw), ("disc", disc), ("d2g", d2g)):
+            for b, lists in d.items():
+                out["ret_%s_%s_len" % (tag, b)] = np.array([len(x) for x in lists], np.int32)
+                out["ret_%s_%s" % (tag, b)] = np.array([v for x in lists for v in x], np.float64)
+        np.savez_compressed(os.path.join(outdir, name + ".npz"), **out)
+        print("eval", name, len(lines), "log lines")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden"))
@@ -589,6 +754,8 @@ def main():
         gen_dsrnn(args.out)
     if want("ppo"):
         gen_ppo(args.out)
+    if want("eval"):
+        gen_eval(args.out)
 
 
 if __name__ == "__main__":
