@@ -55,12 +55,12 @@ __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 // launch geometry + LDS plan of kernel A
 // ------------------------------------------------------------------------------------------------
 struct StepPlan {
-    int T;       // threads per workgroup (256; 128 when N > 12 so the kd-tree path's LDS lines fit)
-    int H;       // human-lane stride: 64 on the quad path (humans in wave 0), T on the kd-tree path
+    int T;       // threads per workgroup (256)
+    int H;       // human-lane stride (64: the humans of EPB envs sit on wave 0's lanes)
     int EPB;     // envs per workgroup
     int M;       // observed slots per human (ORCA lines upper bound)
     int A;       // agents per RVO2 simulator
-    int kd;      // A > 10: KdTree ordering needed
+    int kd;      // A > 10: RVO2's KdTree order decides ties between equally distant neighbours
     // LDS byte offsets
     int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_vis, o_nv, o_lines, o_proj, o_nd, o_ns, o_perm,
         total;
@@ -79,12 +79,13 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.A = N + (robot_visible ? 1 : 0);
     p.M = p.A - 1;
     p.kd = p.A > 10;
-    // quad path (A <= 10): 4 waves, the humans of EPB envs on wave 0's lanes for the per-human phases,
-    // all 256 lanes (4 per human) for ORCA. kd-tree path: one lane per human throughout.
-    p.T = p.kd ? (N > 12 ? 128 : CN_BLK) : CN_BLK;
-    p.H = p.kd ? p.T : 64;
+    // 4 waves: the humans of EPB = 64 / N envs on wave 0's lanes for the per-human phases, the env lanes
+    // on wave 1, all 256 lanes (4 per human) for ORCA. A > 10 adds the KdTree build / query (one lane of
+    // each quad) that fixes RVO2's neighbour order.
+    p.T = CN_BLK;
+    p.H = 64;
     p.EPB = p.H / N;
-    const int H = p.H, T = p.T;
+    const int H = p.H;
     const int ML = p.M > 0 ? p.M : 1;
     int o = 0;
     p.o_renv = o;  o = cn_align16(o + CN_RENV_F * p.EPB * 8);
@@ -96,13 +97,14 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_orad = o;  o = cn_align16(o + H * 4);
     p.o_vis = o;   o = cn_align16(o + 3 * H * 4);          // visible mask, dummy mask, frozen max speed
     p.o_nv = o;    o = cn_align16(o + H * 16);             // new velocity (double2)
-    // ORCA lines: kd path [M][T] per lane; quad path [H][M] per human (sorted lines, projected lines, distSq)
-    p.o_lines = o; o = cn_align16(o + ML * (p.kd ? T : H) * 16);
-    p.o_proj = o;  o = cn_align16(o + ML * (p.kd ? T : H) * 16);
-    p.o_nd = o;    o = cn_align16(o + ML * (p.kd ? T : H) * 4);
-    p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * T : 0));
-    p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * T : 0));
-    p.rng_waves = p.kd ? T / 64 : 4;
+    // ORCA, per human: sorted lines [H][M], projected lines [H][M], neighbour distances; kd: neighbour
+    // slots, KdTree agent order
+    p.o_lines = o; o = cn_align16(o + ML * H * 16);
+    p.o_proj = o;  o = cn_align16(o + ML * H * 16);
+    p.o_nd = o;    o = cn_align16(o + ML * H * 4);
+    p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * H : 0));
+    p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * H : 0));
+    p.rng_waves = 4;
     const int rng_end = p.o_lines + p.rng_waves * CN_PEND_LDS;
     p.total = o > rng_end ? o : rng_end;
     return p;
@@ -567,6 +569,20 @@ __device__ __forceinline__ int quad_or(int x)
 {
     x |= quad_xor1i(x);
     return x | quad_xor2i(x);
+}
+
+// min / max over aligned groups of 8 lanes (quad, then row_half_mirror across the two quads; exact)
+__device__ __forceinline__ float oct_min(float x)
+{
+    x = quad_min(x);
+    const float y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false));
+    return y < x ? y : x;
+}
+__device__ __forceinline__ float oct_max(float x)
+{
+    x = quad_max(x);
+    const float y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false));
+    return x < y ? y : x;
 }
 
 // linearProgram1 on line `no` of Lb (valid lines: bits of vmask), quad-cooperative
@@ -1420,24 +1436,6 @@ __device__ inline void slot_agent(const SL &sl, const cn_config &c, int eb, int 
     }
 }
 
-// RVO2 Agent::insertAgentNeighbor into the lane's sorted (distSq, slot) list in LDS
-__device__ inline void insert_nbr(const SL &sl, int tid, int &cnt, int maxN, int slot, float distSq, float &rangeSq)
-{
-    if (distSq < rangeSq) {
-        if (cnt < maxN) ++cnt;
-        int q = cnt - 1;
-        const int T = sl.T;
-        while (q != 0 && distSq < sl.nd[(q - 1) * T + tid]) {
-            sl.nd[q * T + tid] = sl.nd[(q - 1) * T + tid];
-            sl.ns[q * T + tid] = sl.ns[(q - 1) * T + tid];
-            --q;
-        }
-        sl.nd[q * T + tid] = distSq;
-        sl.ns[q * T + tid] = (uint8_t)slot;
-        if (cnt == maxN) rangeSq = sl.nd[(cnt - 1) * T + tid];
-    }
-}
-
 __device__ inline float bbox_dist(float x, float y, float mnx, float mxx, float mny, float mxy)
 {
     const float a = (0.0f < mnx - x) ? mnx - x : 0.0f, b = (0.0f < x - mxx) ? x - mxx : 0.0f;
@@ -1486,7 +1484,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     const int gh = (e0 + el) * N + i;                 // global human index (E*N < 2^31, cn_config_validate)
     // env lanes (robot / reward / bookkeeping): wave 1 on the quad path, so they run beside the human
     // lanes of wave 0 in phases 0, 3 and 4; the first lanes on the kd-tree path
-    const int re = KD ? tid : tid - 64;
+    const int re = tid - 64;
     const bool rl = re >= 0 && re < nenv_here;
     const int ge = e0 + re;
     const bool holo = c.kinematics == CN_HOLONOMIC;
@@ -1629,12 +1627,8 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     };
     // ---- phase 1: visibility of the other agents to human i, frozen simulator parameters --------
     // (quad path: wave 1 computes the per-human reward terms, wave 2 the robot terms meanwhile)
-    if constexpr (!KD) {
-        if (tid >= 64 && tid - 64 < nenv_here * N) reward_terms(tid - 64);
-        if (tid >= 128 && tid - 128 < nenv_here) robot_terms(tid - 128);
-    } else {
-        if (rl) robot_terms(re);
-    }
+    if (tid >= 64 && tid - 64 < nenv_here * N) reward_terms(tid - 64);
+    if (tid >= 128 && tid - 128 < nenv_here) robot_terms(tid - 128);
     const bool orca = c.human_policy == CN_POLICY_ORCA;
     uint32_t vis = 0, dm = 0;
     float my_vmax = 0.0f;
@@ -1688,16 +1682,23 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     __syncthreads();
     STAMP_A(2);
 
-    // ---- phase 2: human policy (PRE-move state) + per-human reward terms -------------------------
+    // ---- phase 2: human policy (PRE-move state) -------------------------------------------------
     double nvx = 0.0, nvy = 0.0;
-    if constexpr (!KD) {
+    {
         const int nh = nenv_here * N;
         if (orca) {
-            // ORCA.predict for every human (orca.py:64-139), a quad of lanes per human. <= 10 agents: the
-            // KdTree is one leaf, so the neighbour list is the in-range slots stably sorted by distSq
-            // (Agent::insertAgentNeighbor). Lane sq builds the lines of slots sq, sq+4, sq+8.
+            // ORCA.predict for every human (orca.py:64-139), a quad of lanes per human. The neighbour list
+            // (Agent::insertAgentNeighbor with maxNeighbors = M: every agent within neighborDist) is the
+            // in-range slots stably sorted by distSq in the order RVO2's KdTree visits them. <= 10 agents:
+            // one leaf, so that order is the simulator's agents_ order = slot order, and lane sq builds the
+            // lines of slots sq, sq+4, sq+8 and ranks them itself. > 10 agents: lane 0 of the quad runs the
+            // KdTree build (which also re-permutes the persisted agents_ order) and query, the quad then
+            // builds the lines in neighbour order.
             const int h = tid >> 2, sq = tid & 3;
-            if (h < nh) {
+            {
+                // lanes of quads past the last human (h >= nh) stay in step for the KdTree walk (whole
+                // waves) and skip the per-human work; their LDS reads stay inside the [H] arrays
+                const bool hq = h < nh;
                 const int elq = h / N, iq = h - elq * N, eb = elq * N;
                 const uint32_t visq = sl.vis[h], dmq = sl.dm[h];
                 const double px = HF(sl, H_PX, h), py = HF(sl, H_PY, h);
@@ -1712,48 +1713,285 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 double gdx = HF(sl, H_GX, h) - px, gdy = HF(sl, H_GY, h) - py;
                 const double speed = np_norm2(gdx, gdy);
                 if (speed > 1.0) { gdx = ddiv(gdx, speed); gdy = ddiv(gdy, speed); }
-                float *D = sl.nd + h * M;
                 float4 *Lb = sl.lines + h * M, *Pb = sl.proj + h * M;
+                int cnt = 0;
                 uint32_t inm = 0;
-                float4 rawv[3];
-                float dv[3];
+                if constexpr (!KD) {
+                  if (hq) {
+                    float *D = sl.nd + h * M;
+                    float4 rawv[3];
+                    float dv[3];
 #pragma unroll
-                for (int u = 0; u < 3; ++u) {
-                    const int k = sq + 4 * u;
-                    rawv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    dv[u] = 0.0f;
-                    if (k < M) {
+                    for (int u = 0; u < 3; ++u) {
+                        const int k = sq + 4 * u;
+                        rawv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        dv[u] = 0.0f;
+                        if (k < M) {
+                            float x, y, vx, vy, r;
+                            slot_agent(sl, c, eb, elq, EPB, N, iq, k, visq, dmq, rdummy, x, y, vx, vy, r);
+                            const float dx = X0 - x, dy = Y0 - y;
+                            dv[u] = dx * dx + dy * dy;
+                            if (dv[u] < rangeSq) inm |= 1u << k;
+                            rawv[u] = orca_line(X0, Y0, VX0, VY0, R0, x, y, vx, vy, r, invTH, invTS);
+                            D[k] = dv[u];
+                        }
+                    }
+                    inm = (uint32_t)quad_or((int)inm);
+                    wsync();
+#pragma unroll
+                    for (int u = 0; u < 3; ++u) {
+                        const int k = sq + 4 * u;
+                        if (k < M && ((inm >> k) & 1u)) {
+                            int rank = 0;
+                            for (int q = 0; q < M; ++q)
+                                if (((inm >> q) & 1u) && (D[q] < dv[u] || (D[q] == dv[u] && q < k))) ++rank;
+                            Lb[rank] = rawv[u];
+                        }
+                    }
+                    cnt = __popc(inm);
+                  }
+                } else {
+                    // (1) the quad loads the persisted KdTree order and fills, in that order, the agents'
+                    //     positions (XYP[q] = agent perm[q]: self = 0, slot k = k + 1; kept in the projected-
+                    //     lines space, unused until linearProgram3) and each slot's distSq
+                    const int HS = sl.T;   // LDS stride of the per-human slot / KdTree order arrays
+                    float *D = sl.nd + h * M;
+                    float2 *XYP = (float2 *)Pb;
+                    uint8_t *perm = sl.perm, *tpos = sl.ns;
+                    const bool frz = (sl.rflag[elq] & CN_FLAG_ORCA_FROZEN) != 0;
+                    const int gq = (e0 + elq) * N + iq;
+                    for (int q = sq; q < A && hq; q += 4) {
+                        const int a = frz ? S.o_perm[gq * A + q] : q;
+                        perm[q * HS + h] = (uint8_t)a;
+                        if (a == 0) { XYP[q] = make_float2(X0, Y0); continue; }
                         float x, y, vx, vy, r;
-                        slot_agent(sl, c, eb, elq, EPB, N, iq, k, visq, dmq, rdummy, x, y, vx, vy, r);
+                        slot_agent(sl, c, eb, elq, EPB, N, iq, a - 1, visq, dmq, rdummy, x, y, vx, vy, r);
+                        XYP[q] = make_float2(x, y);
                         const float dx = X0 - x, dy = Y0 - y;
-                        dv[u] = dx * dx + dy * dy;
-                        if (dv[u] < rangeSq) inm |= 1u << k;
-                        rawv[u] = orca_line(X0, Y0, VX0, VY0, R0, x, y, vx, vy, r, invTH, invTS);
-                        D[k] = dv[u];
+                        D[a - 1] = dx * dx + dy * dy;
+                        if (D[a - 1] < rangeSq) inm |= 1u << (a - 1);
                     }
-                }
-                inm = (uint32_t)quad_or((int)inm);
-                wsync();
+                    inm = (uint32_t)quad_or((int)inm);
+                    wsync();
+                    STAMP_A(15);
+                    // (2) KdTree build (buildAgentTreeRecursive, which re-permutes the persisted agents_ order)
+                    //     fused with the query's depth-first walk (queryAgentTreeRecursive: closer child first,
+                    //     ties -> right). 8 lanes per human (lane sub holds positions sub, sub+8, sub+16,
+                    //     sub+24 of the agent order), 8 humans per wave at a time. Every node is partitioned
+                    //     once: Hoare's two-pointer loop swaps the i-th element >= split left of the cut with the
+                    //     i-th element < split counted from the right end, which ballots and popcounts give
+                    //     directly (exchange through the human's projected-lines space). The children's
+                    //     bounding boxes (exact min / max over the 8 lanes) give both the visiting order and
+                    //     their own split. Pruned subtrees hold no agent within range, so walking them inserts
+                    //     nothing: the in-range agents' visiting order tpos is the order
+                    //     Agent::insertAgentNeighbor sees. The explicit stack (<= A - 9 entries) lives in the
+                    //     sorted-lines space, written only after the walk.
+                    {
+                        const int lane = tid & 63, grp = lane >> 3, sub = lane & 7;
+                        const int wbase = (tid >> 6) * 16;
+                        auto gmask = [&](const bool (&pr)[4]) -> uint32_t {
+                            uint32_t m = 0;
 #pragma unroll
-                for (int u = 0; u < 3; ++u) {
-                    const int k = sq + 4 * u;
-                    if (k < M && ((inm >> k) & 1u)) {
-                        int rank = 0;
-                        for (int q = 0; q < M; ++q)
-                            if (((inm >> q) & 1u) && (D[q] < dv[u] || (D[q] == dv[u] && q < k))) ++rank;
-                        Lb[rank] = rawv[u];
+                            for (int u = 0; u < 4; ++u)
+                                m |= (uint32_t)((__ballot(pr[u]) >> (8 * grp)) & 0xffull) << (8 * u);
+                            return m;
+                        };
+                        for (int r = 0; r < 2; ++r) {
+                            const int hw = wbase + grp + 8 * r;
+                            if (hw >= nh) continue;
+                            const int elw = hw / N, iw = hw - elw * N;
+                            const int gw = (e0 + elw) * N + iw;
+                            const float *Dw = sl.nd + hw * M;
+                            int4 *stk = (int4 *)(sl.lines + hw * M);
+                            float *xch = (float *)(sl.proj + hw * M);   // 2 x (A / 2) entries of (x, y, a)
+                            const float SX = (float)HF(sl, H_PX, hw), SY = (float)HF(sl, H_PY, hw);
+                            float px[4], py[4];
+                            int pa[4], qq[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                qq[u] = sub + 8 * u;
+                                const bool v = qq[u] < A;
+                                const float2 t = v ? ((const float2 *)xch)[qq[u]] : make_float2(0.0f, 0.0f);
+                                px[u] = t.x; py[u] = t.y;
+                                pa[u] = v ? perm[qq[u] * HS + hw] : 0;
+                            }
+                            auto red = [&](int b0, int e1, float &mnx, float &mxx, float &mny, float &mxy) {
+                                float a0 = INFINITY, a1 = -INFINITY, c0 = INFINITY, c1 = -INFINITY;
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    if (qq[u] >= b0 && qq[u] < e1) {
+                                        a1 = a1 < px[u] ? px[u] : a1; a0 = px[u] < a0 ? px[u] : a0;
+                                        c1 = c1 < py[u] ? py[u] : c1; c0 = py[u] < c0 ? py[u] : c0;
+                                    }
+                                }
+                                mnx = oct_min(a0); mxx = oct_max(a1); mny = oct_min(c0); mxy = oct_max(c1);
+                            };
+                            // z: bit 0 = split on x, bit 1 = all points coincide (zero-extent box)
+                            auto entry = [&](int b0, int e1, float mnx, float mxx, float mny, float mxy) {
+                                const bool vert = (mxx - mnx > mxy - mny);
+                                const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
+                                const int deg = (mnx == mxx && mny == mxy) ? 2 : 0;
+                                return make_int4(b0, e1, (vert ? 1 : 0) | deg, __float_as_int(split));
+                            };
+                            int sp = 0, tc = 0;
+#ifdef CN_STAMPS
+                            int dbg_it = 0;
+#endif
+                            {
+                                float mnx, mxx, mny, mxy;
+                                red(0, A, mnx, mxx, mny, mxy);
+                                stk[0] = entry(0, A, mnx, mxx, mny, mxy);
+                                sp = 1;
+                            }
+                            while (sp > 0) {
+#ifdef CN_STAMPS
+                                ++dbg_it;
+#endif
+                                const int4 en = stk[--sp];
+                                const int b0 = en.x, e1 = en.y;
+                                bool pr[4];
+                                if (e1 - b0 <= 10) {   // leaf (RVO_MAX_LEAF_SIZE): insert in position order
+#pragma unroll
+                                    for (int u = 0; u < 4; ++u)
+                                        pr[u] = qq[u] >= b0 && qq[u] < e1 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
+                                    const uint32_t bits = gmask(pr);
+#pragma unroll
+                                    for (int u = 0; u < 4; ++u)
+                                        if (pr[u])
+                                            tpos[(pa[u] - 1) * HS + hw] =
+                                                (uint8_t)(tc + __popc(bits & ((1u << qq[u]) - 1u)));
+                                    tc += __popc(bits);
+                                    continue;
+                                }
+                                if (en.z & 2) {
+                                    // coincident points (e.g. the dummies of unseen humans, all at (7, 7)): no
+                                    // split separates them, so each level peels its first element into a
+                                    // one-agent leaf, nothing moves, and the equal-distance children are
+                                    // visited right first: positions [e1-10, e1) in order, then e1-11 down to b0
+#pragma unroll
+                                    for (int u = 0; u < 4; ++u)
+                                        pr[u] = qq[u] >= e1 - 10 && qq[u] < e1 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
+                                    const uint32_t b1 = gmask(pr);
+                                    bool p2[4];
+#pragma unroll
+                                    for (int u = 0; u < 4; ++u)
+                                        p2[u] = qq[u] >= b0 && qq[u] < e1 - 10 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
+                                    const uint32_t b2 = gmask(p2);
+#pragma unroll
+                                    for (int u = 0; u < 4; ++u) {
+                                        if (pr[u])
+                                            tpos[(pa[u] - 1) * HS + hw] = (uint8_t)(tc + __popc(b1 & ((1u << qq[u]) - 1u)));
+                                        if (p2[u])
+                                            tpos[(pa[u] - 1) * HS + hw] =
+                                                (uint8_t)(tc + __popc(b1) + __popc(b2 >> qq[u] >> 1));
+                                    }
+                                    tc += __popc(b1) + __popc(b2);
+                                    continue;
+                                }
+                                const float split = __int_as_float(en.w);
+                                bool lt[4], pL[4], pR[4];
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    lt[u] = ((en.z & 1) ? px[u] : py[u]) < split;
+                                    pr[u] = qq[u] >= b0 && qq[u] < e1 && lt[u];
+                                }
+                                const int mid = b0 + __popc(gmask(pr));
+#pragma unroll
+                                for (int u = 0; u < 4; ++u) {
+                                    const bool in = qq[u] >= b0 && qq[u] < e1;
+                                    pL[u] = in && qq[u] < mid && !lt[u];
+                                    pR[u] = in && qq[u] >= mid && lt[u];
+                                }
+                                const uint32_t Lm = gmask(pL), Rm = gmask(pR);
+                                if (Lm) {
+                                    const int nsw = __popc(Lm);
+                                    int slot[4];
+#pragma unroll
+                                    for (int u = 0; u < 4; ++u) {
+                                        slot[u] = pL[u] ? __popc(Lm & ((1u << qq[u]) - 1u))
+                                                        : nsw + __popc(Rm >> qq[u] >> 1);
+                                        if (pL[u] || pR[u]) {
+                                            float *o = xch + 3 * slot[u];
+                                            o[0] = px[u]; o[1] = py[u]; o[2] = __int_as_float(pa[u]);
+                                        }
+                                    }
+                                    wsync();
+#pragma unroll
+                                    for (int u = 0; u < 4; ++u) {
+                                        if (pL[u] || pR[u]) {
+                                            const float *o = xch + 3 * (pL[u] ? slot[u] + nsw : slot[u] - nsw);
+                                            px[u] = o[0]; py[u] = o[1]; pa[u] = __float_as_int(o[2]);
+                                        }
+                                    }
+                                    wsync();
+                                }
+                                const int left = mid == b0 ? mid + 1 : mid;
+                                float l0, l1, l2, l3, r0, r1, r2, r3;
+                                red(b0, left, l0, l1, l2, l3);
+                                red(left, e1, r0, r1, r2, r3);
+                                const int4 cl = entry(b0, left, l0, l1, l2, l3), cr = entry(left, e1, r0, r1, r2, r3);
+                                const float dl = bbox_dist(SX, SY, l0, l1, l2, l3);
+                                const float dr = bbox_dist(SX, SY, r0, r1, r2, r3);
+                                if (sub == 0) {
+                                    if (dl < dr) { stk[sp] = cr; stk[sp + 1] = cl; }   // left visited first
+                                    else { stk[sp] = cl; stk[sp + 1] = cr; }
+                                }
+                                sp += 2;
+                                wsync();
+                            }
+#pragma unroll
+                            for (int u = 0; u < 4; ++u)
+                                if (qq[u] < A) S.o_perm[gw * A + qq[u]] = (uint8_t)pa[u];
+#ifdef CN_STAMPS
+                            if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + 13] = dbg_it;
+#endif
+                        }
                     }
+                    wsync();
+                    STAMP_A(14);
+                    if (hq) {
+                    // (3) neighbour rank = stable order of (distSq, visiting order): each lane ranks its slots
+                    //     sq, sq+4, ... in one pass over the in-range slots, then writes their lines
+                    float myD[8];
+                    int myT[8], rk[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int k = sq + 4 * u;
+                        const bool in = k < M && ((inm >> k) & 1u);
+                        myD[u] = in ? D[k] : 0.0f;
+                        myT[u] = in ? tpos[k * HS + h] : 0;
+                        rk[u] = 0;
+                    }
+                    for (uint32_t mq = inm; mq; mq &= mq - 1) {
+                        const int q = __ffs(mq) - 1;
+                        const float dq = D[q];
+                        const int tq = tpos[q * HS + h];
+#pragma unroll
+                        for (int u = 0; u < 8; ++u) rk[u] += (dq < myD[u] || (dq == myD[u] && tq < myT[u])) ? 1 : 0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int k = sq + 4 * u;
+                        if (k < M && ((inm >> k) & 1u)) {
+                            float ox, oy, ovx, ovy, orr;
+                            slot_agent(sl, c, eb, elq, EPB, N, iq, k, visq, dmq, rdummy, ox, oy, ovx, ovy, orr);
+                            Lb[rk[u]] = orca_line(X0, Y0, VX0, VY0, R0, ox, oy, ovx, ovy, orr, invTH, invTS);
+                        }
+                    }
+                    }
+                    cnt = __popc(inm);
                 }
                 wsync();
-                const int cnt = __popc(inm);
-                const float vmq = sl.vmax[h];
-                float rx, ry;
                 STAMP_A(7);
-                const int fail_at = lp2_q(Lb, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
-                STAMP_A(8);
-                if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
-                STAMP_A(9);
-                if (sq == 0) sl.nv[h] = make_double2((double)rx, (double)ry);
+                if (hq) {
+                    const float vmq = sl.vmax[h];
+                    float rx, ry;
+                    const int fail_at = lp2_q(Lb, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
+                    STAMP_A(8);
+                    if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
+                    STAMP_A(9);
+                    if (sq == 0) sl.nv[h] = make_double2((double)rx, (double)ry);
+                }
             }
         } else if (hl) {
             const int eb = el * N;
@@ -1792,181 +2030,6 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         }
         __syncthreads();
         if (hl) { nvx = sl.nv[tid].x; nvy = sl.nv[tid].y; }
-    } else {
-        if (hl) {
-            const int eb = el * N;
-            const double px = HF(sl, H_PX, tid), py = HF(sl, H_PY, tid);
-            const double vx0 = HF(sl, H_VX, tid), vy0 = HF(sl, H_VY, tid);
-            const double rad = HF(sl, H_R, tid), vpref = HF(sl, H_VP, tid);
-            if (orca) {
-                const float rdummy = (float)(c.human_radius + 0.01 + c.orca_safety_space);
-                const float X0 = (float)px, Y0 = (float)py, VX0 = (float)vx0, VY0 = (float)vy0;
-                const float R0 = sl.orad[tid];
-                const float rangeSq = (float)c.orca_neighbor_dist * (float)c.orca_neighbor_dist;
-                const float invTH = fdiv(1.0f, (float)c.orca_time_horizon);
-                const float invTS = fdiv(1.0f, (float)dt);
-                // preferred velocity: unit vector to the goal only if farther than 1 (orca.py:118-122)
-                double gdx = HF(sl, H_GX, tid) - px, gdy = HF(sl, H_GY, tid) - py;
-                const double speed = np_norm2(gdx, gdy);
-                if (speed > 1.0) { gdx = ddiv(gdx, speed); gdy = ddiv(gdy, speed); }
-                float rx, ry;
-                {
-                    float rq = rangeSq;
-                    int cnt = 0;
-                    const int maxN = M;
-                    const int T = sl.T;
-                    // KdTree: persisted agents_ order (identity at simulator creation)
-                    uint8_t *perm = sl.perm;
-                    for (int a = 0; a < A; ++a) perm[a * T + tid] = frozen ? S.o_perm[gh * A + a] : (uint8_t)a;
-                    auto AX = [&](int a) -> float {
-                        if (a == 0) return X0;
-                        float x, y, vx, vy, r;
-                        slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
-                        return x;
-                    };
-                    auto AY = [&](int a) -> float {
-                        if (a == 0) return Y0;
-                        float x, y, vx, vy, r;
-                        slot_agent(sl, c, eb, el, EPB, N, i, a - 1, vis, dm, rdummy, x, y, vx, vy, r);
-                        return y;
-                    };
-                    // build (buildAgentTreeRecursive), iteratively; partitions perm in place
-                    int stb[CN_MAX_A], ste[CN_MAX_A], sp = 0;
-                    stb[sp] = 0; ste[sp] = A; ++sp;
-                    while (sp > 0) {
-                        --sp;
-                        const int b = stb[sp], e = ste[sp];
-                        if (e - b <= 10) continue;
-                        float mnx = AX(perm[b * T + tid]), mxx = mnx;
-                        float mny = AY(perm[b * T + tid]), mxy = mny;
-                        for (int q = b + 1; q < e; ++q) {
-                            const int a = perm[q * T + tid];
-                            const float x = AX(a), y = AY(a);
-                            mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
-                            mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
-                        }
-                        const bool vert = (mxx - mnx > mxy - mny);
-                        const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
-                        int left = b, right = e;
-                        while (left < right) {
-                            while (left < right) {
-                                const int a = perm[left * T + tid];
-                                if (!((vert ? AX(a) : AY(a)) < split)) break;
-                                ++left;
-                            }
-                            while (right > left) {
-                                const int a = perm[(right - 1) * T + tid];
-                                if (!((vert ? AX(a) : AY(a)) >= split)) break;
-                                --right;
-                            }
-                            if (left < right) {
-                                const uint8_t t0 = perm[left * T + tid];
-                                perm[left * T + tid] = perm[(right - 1) * T + tid];
-                                perm[(right - 1) * T + tid] = t0;
-                                ++left; --right;
-                            }
-                        }
-                        if (left == b) { ++left; }
-                        stb[sp] = b; ste[sp] = left; ++sp;
-                        stb[sp] = left; ste[sp] = e; ++sp;
-                    }
-                    for (int a = 0; a < A; ++a) S.o_perm[gh * A + a] = perm[a * T + tid];
-                    // query (queryAgentTreeRecursive): closer child first, ties -> right; subtree pruning
-                    // never drops an in-range agent, so visiting every leaf inserts the same neighbours
-                    sp = 0; stb[sp] = 0; ste[sp] = A; ++sp;
-                    while (sp > 0) {
-                        --sp;
-                        const int b = stb[sp], e = ste[sp];
-                        if (e - b <= 10) {
-                            for (int q = b; q < e; ++q) {
-                                const int a = perm[q * T + tid];
-                                if (a == 0) continue;
-                                const float dx = X0 - AX(a), dy = Y0 - AY(a);
-                                insert_nbr(sl, tid, cnt, maxN, a - 1, dx * dx + dy * dy, rq);
-                            }
-                            continue;
-                        }
-                        float mnx = AX(perm[b * T + tid]), mxx = mnx;
-                        float mny = AY(perm[b * T + tid]), mxy = mny;
-                        for (int q = b + 1; q < e; ++q) {
-                            const int a = perm[q * T + tid];
-                            const float x = AX(a), y = AY(a);
-                            mxx = mxx < x ? x : mxx; mnx = x < mnx ? x : mnx;
-                            mxy = mxy < y ? y : mxy; mny = y < mny ? y : mny;
-                        }
-                        const bool vert = (mxx - mnx > mxy - mny);
-                        const float split = vert ? 0.5f * (mxx + mnx) : 0.5f * (mxy + mny);
-                        int left = b;
-                        for (int q = b; q < e; ++q) {
-                            const int a = perm[q * T + tid];
-                            if ((vert ? AX(a) : AY(a)) < split) ++left;
-                        }
-                        if (left == b) ++left;
-                        float bb[2][4];
-                        for (int ch = 0; ch < 2; ++ch) {
-                            const int cb = ch ? left : b, ce = ch ? e : left;
-                            float a0x = AX(perm[cb * T + tid]), a1x = a0x;
-                            float a0y = AY(perm[cb * T + tid]), a1y = a0y;
-                            for (int q = cb + 1; q < ce; ++q) {
-                                const int a = perm[q * T + tid];
-                                const float x = AX(a), y = AY(a);
-                                a1x = a1x < x ? x : a1x; a0x = x < a0x ? x : a0x;
-                                a1y = a1y < y ? y : a1y; a0y = y < a0y ? y : a0y;
-                            }
-                            bb[ch][0] = a0x; bb[ch][1] = a1x; bb[ch][2] = a0y; bb[ch][3] = a1y;
-                        }
-                        const float dl = bbox_dist(X0, Y0, bb[0][0], bb[0][1], bb[0][2], bb[0][3]);
-                        const float dr = bbox_dist(X0, Y0, bb[1][0], bb[1][1], bb[1][2], bb[1][3]);
-                        if (dl < dr) {  // visit left first: push right, then left
-                            stb[sp] = left; ste[sp] = e; ++sp; stb[sp] = b; ste[sp] = left; ++sp;
-                        } else {
-                            stb[sp] = b; ste[sp] = left; ++sp; stb[sp] = left; ste[sp] = e; ++sp;
-                        }
-                    }
-                    // ORCA lines in neighbour order (Agent::computeNewVelocity, agents only)
-                    LineView L{sl.lines, tid, T}, PL{sl.proj, tid, T};
-                    for (int pq = 0; pq < cnt; ++pq) {
-                        const int k = sl.ns[pq * T + tid];
-                        float ox, oy, ovx, ovy, orr;
-                        slot_agent(sl, c, eb, el, EPB, N, i, k, vis, dm, rdummy, ox, oy, ovx, ovy, orr);
-                        L.set(pq, orca_line(X0, Y0, VX0, VY0, R0, ox, oy, ovx, ovy, orr, invTH, invTS));
-                    }
-                    const int fail_at = lp2(L, cnt, my_vmax, (float)gdx, (float)gdy, rx, ry);
-                    if (fail_at < cnt) lp3(L, PL, cnt, fail_at, my_vmax, rx, ry);
-                }
-                nvx = (double)rx; nvy = (double)ry;
-            } else {
-                // SOCIAL_FORCE.predict (social_force.py:11-66)
-                const double dx = HF(sl, H_GX, tid) - px, dy = HF(sl, H_GY, tid) - py;
-                const double dist = dsqrt(dx * dx + dy * dy);
-                const double dvx = ddiv(dx, dist) * vpref, dvy = ddiv(dy, dist) * vpref;
-                const double cdx = c.sf_KI * (dvx - vx0), cdy = c.sf_KI * (dvy - vy0);
-                double ix = 0.0, iy = 0.0;
-                for (int k = 0; k < M; ++k) {
-                    double ox, oy, orr;
-                    const bool v = (vis >> k) & 1u;
-                    if (k < N - 1) {
-                        const int j = eb + (k < i ? k : k + 1);
-                        ox = v ? HF(sl, H_PX, j) : CN_DUMMY_POS; oy = v ? HF(sl, H_PY, j) : CN_DUMMY_POS;
-                        orr = v ? HF(sl, H_R, j) : c.human_radius;
-                    } else {
-                        ox = v ? RF(sl, R_PX, el, EPB) : CN_DUMMY_POS; oy = v ? RF(sl, R_PY, el, EPB) : CN_DUMMY_POS;
-                        orr = v ? RF(sl, R_RAD, el, EPB) : c.robot_radius;
-                    }
-                    const double ddx = px - ox, ddy = py - oy;
-                    const double d = dsqrt(ddx * ddx + ddy * ddy);
-                    const double ex = exp(ddiv(rad + orr - d, c.sf_B));
-                    ix += c.sf_A * ex * ddiv(ddx, d);
-                    iy += c.sf_A * ex * ddiv(ddy, d);
-                }
-                const double tx = (cdx + ix) * dt, ty = (cdy + iy) * dt;
-                const double nx = vx0 + tx, ny = vy0 + ty;
-                const double n = np_norm2(nx, ny);
-                if (n > vpref) { nvx = ddiv(nx, n) * vpref; nvy = ddiv(ny, n) * vpref; }
-                else { nvx = nx; nvy = ny; }
-            }
-            reward_terms(tid);
-        }
     }
     __syncthreads();
     STAMP_A(3);

@@ -122,6 +122,9 @@ def _teacher_forced(gpu, oracle, cfg, kin, steps=60, seed=5):
     ("unicycle_sf_perp", "unicycle", 5, "social_force", "perpendicular_traffic", {}),
     ("single_human", "holonomic", 1, "orca", "circle_crossing", {}),
     ("two_humans_time_factor", "unicycle", 2, "orca", "circle_crossing", {"reward__time_factor": True}),
+    ("kd_tree_max_agents", "holonomic", 31, "orca", "square_crossing",
+     {"robot__visible": True, "robot__FOV": 1.0, "humans__FOV": 1.0}),
+    ("kd_tree_11_agents", "unicycle", 11, "orca", "circle_crossing", {"humans__FOV": 0.5}),
 ])
 def test_gpu_vs_oracle_configs(gpu, oracle, name, kin, N, policy, scen, over):
     """Teacher-forced GPU vs oracle over the option space the reference exposes (SURVEY §8d C5 shapes,

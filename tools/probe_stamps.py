@@ -1,5 +1,8 @@
 """Diagnostic: phase breakdown of the step and RNG kernels from the -DCN_STAMPS build.
 
+    hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -DCN_STAMPS \
+        -o crowdnav_dsrnn_amd/lib/libcrowdnav_hip_stamps.so crowdnav_dsrnn_amd/csrc/cn_engine.hip crowdnav_dsrnn_amd/csrc/cn_gru.hip
+
     CN_LIB_PATH=crowdnav_dsrnn_amd/lib/libcrowdnav_hip_stamps.so python tools/probe_stamps.py [variant]
 """
 import ctypes
@@ -47,8 +50,7 @@ def run(variant, E=4096, N=10, steps=300):
     ta, tb, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
     L.cn_profile_read(eng._h, ctypes.byref(ta), ctypes.byref(tb), ctypes.byref(n))
     L.cn_debug_stamps(a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p))
-    T = 64 if N <= 10 else (256 if N <= 12 else 128)
-    blocks = (E + (T // N) - 1) // (T // N)
+    blocks = (E + (64 // N) - 1) // (64 // N)
     A = a.reshape(-1, 16)[:blocks].astype(np.int64)
     d = np.diff(A[:, :7], axis=1)
     print("[%s] kernel A avg %.1f us, kernel B avg %.1f us over %d steps" % (variant, ta.value * 1e3 / n.value,
@@ -63,6 +65,13 @@ def run(variant, E=4096, N=10, steps=300):
     t0 = A[:, 0].min()
     sub = [("p0 human loads", A[:, 12] - A[:, 0]), ("p0 env loads", A[:, 13] - A[:, 12]), ("p0 clip", A[:, 10] - A[:, 13]), ("p0 robot VR", A[:, 11] - A[:, 10]), ("p0 barrier", A[:, 1] - A[:, 11]),
            ("lines+sort", A[:, 7] - A[:, 2]), ("LP2", A[:, 8] - A[:, 7]), ("LP3", A[:, 9] - A[:, 8]), ("VR+terms", A[:, 3] - A[:, 9])]
+    if (A[:, 14] > A[:, 2]).all():
+        sub += [("kd: table", A[:, 15] - A[:, 2]), ("kd: walk", A[:, 14] - A[:, 15]),
+                ("kd: rank+lines", A[:, 7] - A[:, 14])]
+    if variant == "c3":
+        it = A[:, 13]
+        print("      kd walk iterations (thread 0's human, round 2): median %d max %d mean %.2f" % (np.median(it), it.max(), it.mean()))
+        sub = [x for x in sub if not x[0].startswith("p0")]
     for nm, v in sub:
         print("      wave0 %-12s median %8d  max %8d" % (nm, np.median(v), v.max()))
     cur = B[:, 0] >= t0                      # items of the last step only
