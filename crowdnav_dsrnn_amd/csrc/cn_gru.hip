@@ -147,3 +147,94 @@ int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_n
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Attention pooling of the spatial edge states (EdgeAttention.forward, srnn_model.py:320-333):
+//   out[r][h] = sum_n hs[r][n][h] * attn[r][n]          (the reference's bmm(hs^T, attn))
+// and its gradient. HBM-bound: one read of hs forward; one read of hs + one write of d_hs backward.
+// One thread per (r, 4 consecutive h); the backward reduces d_attn[r][n] = sum_h dout[r][h] hs[r][n][h]
+// over the row's H / 4 threads with a fixed-order tree (deterministic).
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+__global__ __launch_bounds__(256) void cn_attn_pool_fwd_kernel(int64_t R, int N, int H, const float *__restrict__ hs,
+                                                               const float *__restrict__ attn,
+                                                               float *__restrict__ out)
+{
+    const int H4 = H >> 2;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= R * H4) return;
+    const int64_t r = i / H4;
+    const int j = (int)(i - r * H4) * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int n = 0; n < N; ++n) {
+        const float a = attn[r * N + n];
+        const float4 v = *(const float4 *)(hs + (r * N + n) * H + j);
+        acc.x += v.x * a; acc.y += v.y * a; acc.z += v.z * a; acc.w += v.w * a;
+    }
+    *(float4 *)(out + r * H + j) = acc;
+}
+
+// block = 256 threads = 256 / (H / 4) rows; H / 4 must be a power of two <= 64 (one wave or less per row)
+template <int HQ>
+__global__ __launch_bounds__(256) void cn_attn_pool_bwd_kernel(int64_t R, int N, const float *__restrict__ hs,
+                                                               const float *__restrict__ attn,
+                                                               const float *__restrict__ dout,
+                                                               float *__restrict__ dhs, float *__restrict__ dattn)
+{
+    constexpr int H = HQ * 4;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t r = i / HQ;
+    const int q = (int)(i - r * HQ);
+    const bool ok = r < R;
+    const int j = q * 4;
+    const float4 g = ok ? *(const float4 *)(dout + r * H + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int n = 0; n < N; ++n) {
+        float part = 0.0f;
+        if (ok) {
+            const float a = attn[r * N + n];
+            const float4 v = *(const float4 *)(hs + (r * N + n) * H + j);
+            *(float4 *)(dhs + (r * N + n) * H + j) = make_float4(g.x * a, g.y * a, g.z * a, g.w * a);
+            part = ((g.x * v.x + g.y * v.y) + g.z * v.z) + g.w * v.w;
+        }
+#pragma unroll
+        for (int o = HQ / 2; o; o >>= 1) part += __shfl_xor(part, o);
+        if (ok && q == 0) dattn[r * N + n] = part;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, float *out)
+{
+    if (R <= 0 || N <= 0 || H <= 0 || (H & 3)) return cn_set_error(CN_EINVAL, "cn_attn_pool_fwd: bad shape");
+    if (!hs || !attn || !out) return cn_set_error(CN_EINVAL, "cn_attn_pool_fwd: null operand");
+    hipLaunchKernelGGL(cn_attn_pool_fwd_kernel, dim3(grid_for(R, H)), dim3(256), 0, (hipStream_t)stream, R, N, H, hs,
+                       attn, out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+int cn_attn_pool_bwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, const float *dout,
+                     float *dhs, float *dattn)
+{
+    if (R <= 0 || N <= 0 || !(H == 256 || H == 128 || H == 64))
+        return cn_set_error(CN_EINVAL, "cn_attn_pool_bwd: H must be 64, 128 or 256");
+    if (!hs || !attn || !dout || !dhs || !dattn) return cn_set_error(CN_EINVAL, "cn_attn_pool_bwd: null operand");
+    const unsigned grid = grid_for(R, H);
+    if (H == 256)
+        hipLaunchKernelGGL(cn_attn_pool_bwd_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, hs, attn,
+                           dout, dhs, dattn);
+    else if (H == 128)
+        hipLaunchKernelGGL(cn_attn_pool_bwd_kernel<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, hs, attn,
+                           dout, dhs, dattn);
+    else
+        hipLaunchKernelGGL(cn_attn_pool_bwd_kernel<16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, hs, attn,
+                           dout, dhs, dattn);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+}  // extern "C"

@@ -3,6 +3,7 @@
 edge_features(...)  — the fused DSRNN input layers (cn_edge_features, include/crowdnav.h): one launch
                       computes relu(temporal encoder), relu(spatial encoder) and
                       relu(node encoder(robot_linear(robot_node))) for every env (and time step).
+attention_pool(...) — EdgeAttention's weighted sum of the spatial edge states (cn_attn_pool_*).
 masked_gru(...)     — the mask-segmented GRU of the three DSRNN RNNs over a (T, B) sequence
                       (cn_gru_fwd_step / cn_gru_bwd_step + library GEMMs), with its own backward.
 """
@@ -148,3 +149,39 @@ def masked_gru(x, h0, masks, w_ih, w_hh, b_ih, b_hh):
     if x.dtype != torch.float32 or w_hh.shape[1] % 4:
         raise ValueError("masked_gru: fp32 operands and a hidden size divisible by 4 required")
     return _MaskedGRU.apply(x, h0, masks, w_ih, w_hh, b_ih, b_hh)
+
+
+class _AttnPool(torch.autograd.Function):
+    """srnn_model.py:320-333: weighted = bmm(h_spatials^T, attn) as one HBM pass (cn_attn_pool_fwd) and
+    a one-pass backward (cn_attn_pool_bwd: d h_spatials and d attn together)."""
+
+    @staticmethod
+    def forward(ctx, hs, attn):
+        R, N, H = hs.shape
+        hs, attn = _c(hs), _c(attn).reshape(R, N)
+        out = torch.empty((R, H), dtype=torch.float32, device=hs.device)
+        with torch.cuda.device(hs.device):
+            _lib.check(_lib.lib().cn_attn_pool_fwd(_stream(hs.device), R, N, H, hs.data_ptr(), attn.data_ptr(),
+                                                   out.data_ptr()))
+        ctx.save_for_backward(hs, attn)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        hs, attn = ctx.saved_tensors
+        R, N, H = hs.shape
+        dout = _c(dout)
+        dhs = torch.empty_like(hs)
+        dattn = torch.empty((R, N), dtype=torch.float32, device=hs.device)
+        with torch.cuda.device(hs.device):
+            _lib.check(_lib.lib().cn_attn_pool_bwd(_stream(hs.device), R, N, H, hs.data_ptr(), attn.data_ptr(),
+                                                   dout.data_ptr(), dhs.data_ptr(), dattn.data_ptr()))
+        return dhs, dattn.reshape(R, N, 1)
+
+
+def attention_pool(hs, attn):
+    """hs (R, N, H), attn (R, N, 1) -> (R, H) = sum_n hs[:, n, :] * attn[:, n] (bmm(hs^T, attn))."""
+    if not hs.is_cuda:
+        raise EdgeFeaturesUnavailable("the DSRNN attention pooling runs only as the HIP kernel (cn_attn_pool_*); "
+                                      "tensors are on %s" % hs.device)
+    return _AttnPool.apply(hs, attn)

@@ -107,7 +107,7 @@ class EdgeAttention(nn.Module):
         attn = (spatial_embed * temporal_embed.unsqueeze(2)).sum(-1)      # (T,B,N)
         attn = attn * (N / np.sqrt(self.attention_size))                  # temperature = num_edges / sqrt(d)
         attn = torch.softmax(attn, dim=-1).reshape(T * B, N, 1)
-        weighted = torch.bmm(h_spatials.reshape(T * B, N, H).transpose(1, 2), attn)  # (T*B, H, 1)
+        weighted = ops.attention_pool(h_spatials.reshape(T * B, N, H), attn)  # bmm(hs^T, attn): (T*B, H)
         return weighted.reshape(T, B, H), attn
 
 

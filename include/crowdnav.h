@@ -22,6 +22,8 @@
  *   cn_gru_fwd_step / cn_gru_bwd_step ⟵ one time step of the mask-segmented GRU
  *                   (srnn_model.py:52-104 RNNBase._forward_gru, torch nn.GRU cell math) and its gradient;
  *                   the GEMMs around them (x W_ih^T, hm W_hh^T, dgh W_hh) are library GEMMs
+ *   cn_attn_pool_fwd / cn_attn_pool_bwd ⟵ EdgeAttention's weighted sum of the spatial edge states
+ *                   (srnn_model.py:320-333, torch.bmm(h_spatials^T, attn)) and its gradient
  *
  * Conventions
  *   - All array arguments are DEVICE pointers (torch tensors' data_ptr()), row-major, caller-owned.
@@ -195,6 +197,14 @@ int cn_gru_fwd_step(void *stream, int64_t B, int H, const float *gi, const float
  * acc <- dL/dh_t * z (the caller then adds dgh W_hh to obtain dL/dhm_t). */
 int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
                     const float *save, const float *hm, float *dgi, float *dgh);
+
+/* out[r][h] = sum_n hs[r][n][h] * attn[r][n]; hs [R][N][H], attn [R][N], out [R][H]; H % 4 == 0. */
+int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, float *out);
+
+/* Gradient of cn_attn_pool_fwd: dhs[r][n][h] = dout[r][h] * attn[r][n],
+ * dattn[r][n] = sum_h dout[r][h] * hs[r][n][h] (fixed-order reduction). H in {64, 128, 256}. */
+int cn_attn_pool_bwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, const float *dout,
+                     float *dhs, float *dattn);
 
 #ifdef __cplusplus
 }

@@ -221,3 +221,10 @@ def masked_gru_ref(x, h0, masks, w_ih, w_hh, b_ih, b_hh):
         h = torch.gru_cell(x[t], h * masks[t].unsqueeze(-1), w_ih, w_hh, b_ih, b_hh)
         outs.append(h)
     return torch.stack(outs, 0), h
+
+
+def attention_pool_ref(hs, attn):
+    """Plain PyTorch restatement of EdgeAttention's weighted sum (srnn_model.py:320-333)."""
+    import torch
+
+    return torch.bmm(hs.transpose(1, 2), attn).squeeze(-1)

@@ -11,7 +11,7 @@ import torch
 
 from crowdnav_dsrnn_amd.learner import PPO, SRNNRolloutStorage
 from crowdnav_dsrnn_amd.spaces import Box
-from tests.helpers import edge_features_fp32, masked_gru_ref, load, make_policy
+from tests.helpers import attention_pool_ref, edge_features_fp32, masked_gru_ref, load, make_policy
 
 N, E, T = 5, 4, 8
 
@@ -108,6 +108,7 @@ def test_ppo_update_cpu(fx, monkeypatch):
 
     monkeypatch.setattr(ops, "edge_features", edge_features_fp32)
     monkeypatch.setattr(ops, "masked_gru", masked_gru_ref)
+    monkeypatch.setattr(ops, "attention_pool", attention_pool_ref)
     pol, losses = _update(fx, "cpu")
     np.testing.assert_allclose(losses, fx["update_losses"], atol=2e-6, rtol=1e-5)
     for k, v in pol.state_dict().items():
@@ -129,6 +130,7 @@ def _dist_worker(rank, world, port, out):
 
     ops.edge_features = edge_features_fp32
     ops.masked_gru = masked_gru_ref
+    ops.attention_pool = attention_pool_ref
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from tests.helpers import edge_features_fp32, masked_gru_ref, load, make_policy
+from tests.helpers import attention_pool_ref, edge_features_fp32, masked_gru_ref, load, make_policy
 
 ATOL, RTOL = 2e-5, 1e-4
 
@@ -89,6 +89,7 @@ def test_policy_graph_cpu_with_fp32_input_layers(dsrnn, N, monkeypatch):
 
     monkeypatch.setattr(ops, "edge_features", edge_features_fp32)
     monkeypatch.setattr(ops, "masked_gru", masked_gru_ref)
+    monkeypatch.setattr(ops, "attention_pool", attention_pool_ref)
     _check_act(dsrnn, N, _run_act(dsrnn, N, "cpu"))
     _check_eval(dsrnn, N, _run_eval(dsrnn, N, "cpu"))
 
@@ -171,3 +172,27 @@ def test_masked_gru_kernels_vs_fp64(T, B, F, H):
     for n, a, b in zip(names, got, want):
         tol = 2e-5 if n in ("out", "hT") else 1e-4 * max(1.0, float(b.abs().max()))
         np.testing.assert_allclose(a.numpy(), b.numpy(), atol=tol, rtol=0, err_msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,N,H", [(1, 1, 256), (37, 10, 256), (300, 25, 128), (5, 3, 64)])
+def test_attention_pool_kernels_vs_fp64(R, N, H):
+    """cn_attn_pool_fwd / _bwd vs bmm(hs^T, attn) in float64 (srnn_model.py:320-333): output and both
+    gradients; fp32 summation over N (forward) / H (d attn): atol 1e-5 x scale."""
+    from crowdnav_dsrnn_amd import ops
+
+    g = torch.Generator().manual_seed(R * 7 + N)
+    hs = torch.randn(R, N, H, generator=g)
+    attn = torch.softmax(torch.randn(R, N, generator=g), -1).reshape(R, N, 1)
+    dout = torch.randn(R, H, generator=g)
+
+    def run(fn, dev, dt):
+        a, b = hs.to(dev, dt).requires_grad_(True), attn.to(dev, dt).requires_grad_(True)
+        out = fn(a, b)
+        (out * dout.to(dev, dt)).sum().backward()
+        return [x.detach().cpu().double() for x in (out, a.grad, b.grad)]
+
+    got = run(ops.attention_pool, "cuda:0", torch.float32)
+    want = run(attention_pool_ref, "cpu", torch.float64)
+    for n, a, b in zip(("out", "d_hs", "d_attn"), got, want):
+        np.testing.assert_allclose(a.numpy(), b.numpy(), atol=1e-5 * max(1.0, float(b.abs().max())), rtol=0, err_msg=n)

@@ -61,6 +61,11 @@ def run(variant, E=4096, N=10, steps=300):
     for k, nm in enumerate(names):
         print("    %-26s median %8d  max %8d  (%.0f%%)" % (nm, np.median(d[:, k]), d[:, k].max(),
                                                             100 * np.median(d[:, k]) / np.median(tot)))
+    slow = tot >= np.percentile(tot, 95)
+    print("  slowest 5%% workgroups (total >= %d): mean per phase %s" % (
+        np.percentile(tot, 95), ", ".join("%s %d" % (nm.split()[0], d[slow, k].mean()) for k, nm in enumerate(names))))
+    span = A[:, 6].max() - A[:, 0].min()
+    print("  launch span (first start -> last end) %d cycles; start skew max %d" % (span, A[:, 0].max() - A[:, 0].min()))
     B = b.reshape(-1, 16).astype(np.int64)[:E]
     t0 = A[:, 0].min()
     sub = [("p0 human loads", A[:, 12] - A[:, 0]), ("p0 env loads", A[:, 13] - A[:, 12]), ("p0 clip", A[:, 10] - A[:, 13]), ("p0 robot VR", A[:, 11] - A[:, 10]), ("p0 barrier", A[:, 1] - A[:, 11]),
