@@ -3,6 +3,8 @@
 edge_features(...)  — the fused DSRNN input layers (cn_edge_features, include/crowdnav.h): one launch
                       computes relu(temporal encoder), relu(spatial encoder) and
                       relu(node encoder(robot_linear(robot_node))) for every env (and time step).
+linear(...)         — nn.Linear with a split-K weight gradient (library GEMMs; for the layers applied to
+                      T*B or T*B*N rows in training, where dW = dY^T X has a tiny output and K ~ 10^6).
 attention_pool(...) — EdgeAttention's weighted sum of the spatial edge states (cn_attn_pool_*).
 masked_gru(...)     — the mask-segmented GRU of the three DSRNN RNNs over a (T, B) sequence
                       (cn_gru_fwd_step / cn_gru_bwd_step + library GEMMs), with its own backward.
@@ -75,6 +77,45 @@ def edge_features(robot_node, temporal, spatial, Wt, bt, Ws, bs, Wr, br, Wn, bn)
     return _EdgeFeatures.apply(robot_node, temporal, spatial, Wt, bt, Ws, bs, Wr, br, Wn, bn)
 
 
+def wgrad(dy, x, chunk=16384):
+    """dy^T @ x for (K, m), (K, n) with K >> m, n: K split into S chunks (one batched GEMM, then a sum over
+    S) so the reduction fills the GPU instead of m*n/tile workgroups walking all of K."""
+    K = dy.shape[0]
+    S = K // chunk
+    if S < 4:
+        return dy.t() @ x
+    Kc = K // S
+    main = torch.bmm(dy[:S * Kc].view(S, Kc, -1).transpose(1, 2), x[:S * Kc].view(S, Kc, -1)).sum(0)
+    if S * Kc < K:
+        main = main + dy[S * Kc:].t() @ x[S * Kc:]
+    return main
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch.addmm(b, x2, W.t()) if b is not None else x2 @ W.t()
+        ctx.save_for_backward(x2, W)
+        ctx.has_b = b is not None
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], W.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, W = ctx.saved_tensors
+        dy2 = dy.reshape(-1, W.shape[0]).contiguous()
+        dx = (dy2 @ W).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dW = wgrad(dy2, x2) if ctx.needs_input_grad[1] else None
+        db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        return dx, dW, db
+
+
+def linear(x, W, b=None):
+    """y = x W^T + b (torch.nn.functional.linear) with the split-K weight gradient."""
+    return _Linear.apply(x, W, b)
+
+
 class _MaskedGRU(torch.autograd.Function):
     """srnn_model.py:52-104 (RNNBase._forward_gru): h <- h * mask[t] before step t, then one nn.GRU step.
 
@@ -138,7 +179,7 @@ class _MaskedGRU(torch.autograd.Function):
         dgi2 = dgi.reshape(T * B, 3 * H)
         dgh2 = dgh.reshape(T * B, 3 * H)
         dx = (dgi2 @ w_ih).reshape(T, B, -1) if ctx.needs_input_grad[0] else None
-        return (dx, dh0, None, dgi2.t() @ x2, dgh2.t() @ hm.reshape(T * B, H), dgi2.sum(0), dgh2.sum(0))
+        return (dx, dh0, None, wgrad(dgi2, x2), wgrad(dgh2, hm.reshape(T * B, H)), dgi2.sum(0), dgh2.sum(0))
 
 
 def masked_gru(x, h0, masks, w_ih, w_hh, b_ih, b_hh):

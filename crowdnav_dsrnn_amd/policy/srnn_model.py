@@ -18,7 +18,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from .utils import init
+from .utils import Linear, init
 
 
 class RNNBase(nn.Module):
@@ -58,8 +58,8 @@ class HumanNodeRNN(RNNBase):
         self.encoder_linear = nn.Linear(self.input_size, self.embedding_size)
         self.relu = nn.ReLU()
         self.edge_embed = nn.Linear(self.edge_rnn_size, self.embedding_size)  # unused by forward (kept for keys)
-        self.edge_attention_embed = nn.Linear(self.edge_rnn_size * 2, self.embedding_size)
-        self.output_linear = nn.Linear(self.rnn_size, self.output_size)
+        self.edge_attention_embed = Linear(self.edge_rnn_size * 2, self.embedding_size)
+        self.output_linear = Linear(self.rnn_size, self.output_size)
 
     def forward(self, node_embed, h_temporal, h_spatial_other, h, masks):
         """node_embed (T,B,64) = relu(encoder_linear(robot_linear(robot_node))) from the fused kernel."""
@@ -94,8 +94,8 @@ class EdgeAttention(nn.Module):
         self.human_human_edge_rnn_size = config.SRNN.human_human_edge_rnn_size
         self.human_node_rnn_size = config.SRNN.human_node_rnn_size
         self.attention_size = config.SRNN.attention_size
-        self.temporal_edge_layer = nn.ModuleList([nn.Linear(self.human_human_edge_rnn_size, self.attention_size)])
-        self.spatial_edge_layer = nn.ModuleList([nn.Linear(self.human_human_edge_rnn_size, self.attention_size)])
+        self.temporal_edge_layer = nn.ModuleList([Linear(self.human_human_edge_rnn_size, self.attention_size)])
+        self.spatial_edge_layer = nn.ModuleList([Linear(self.human_human_edge_rnn_size, self.attention_size)])
         self.agent_num = 1
         self.num_attention_head = 1
 
@@ -136,11 +136,11 @@ class SRNN(nn.Module):
             return init(m, nn.init.orthogonal_, lambda x: nn.init.constant_(x, 0), np.sqrt(2))
 
         num_inputs = hidden_size = self.output_size
-        self.actor = nn.Sequential(init_(nn.Linear(num_inputs, hidden_size)), nn.Tanh(),
-                                   init_(nn.Linear(hidden_size, hidden_size)), nn.Tanh())
-        self.critic = nn.Sequential(init_(nn.Linear(num_inputs, hidden_size)), nn.Tanh(),
-                                    init_(nn.Linear(hidden_size, hidden_size)), nn.Tanh())
-        self.critic_linear = init_(nn.Linear(hidden_size, 1))
+        self.actor = nn.Sequential(init_(Linear(num_inputs, hidden_size)), nn.Tanh(),
+                                   init_(Linear(hidden_size, hidden_size)), nn.Tanh())
+        self.critic = nn.Sequential(init_(Linear(num_inputs, hidden_size)), nn.Tanh(),
+                                    init_(Linear(hidden_size, hidden_size)), nn.Tanh())
+        self.critic_linear = init_(Linear(hidden_size, 1))
         self.robot_linear = init_(nn.Linear(7, 3))
         self.human_node_final_linear = init_(nn.Linear(self.output_size, 2))  # unused by forward (keys)
         self.num_edges = self.human_num + 1

@@ -29,3 +29,13 @@ def update_linear_schedule(optimizer, epoch, total_num_epochs, initial_lr):
     lr = initial_lr - (initial_lr * (epoch / float(total_num_epochs)))
     for param_group in optimizer.param_groups:
         param_group["lr"] = lr
+
+
+class Linear(nn.Linear):
+    """nn.Linear (same parameters and state_dict keys) whose training backward uses a split-K weight
+    gradient (ops.linear): these layers see T*B or T*B*N rows in PPO minibatches."""
+
+    def forward(self, x):
+        from .. import ops
+
+        return ops.linear(x, self.weight, self.bias)
