@@ -179,14 +179,15 @@ def make_cn_config(config, num_envs, env_offset=0, nenv=None, phase=None, seed=N
         bad.append("humans.random_policy_changing (uses the unseeded python random module)")
     if getattr(config.noise, "add_noise", False):
         bad.append("noise.add_noise")
-    if getattr(config.lidar, "enable", False):
-        bad.append("lidar.enable (LiDAR/ConvGRU path is out of scope)")
+    # lidar.enable: the LiDAR scan only feeds the 'convgru' observation, built outside the step kernel by
+    # cn_lidar_obs (CrowdNavVecEnv); with the srnn policy it changes nothing the reference returns
     if not config.reward.potential_based or getattr(config.reward, "exponential", False):
         bad.append("reward.exponential")
     if config.humans.policy not in ("orca", "social_force"):
         bad.append("humans.policy=%r" % config.humans.policy)
-    if config.robot.policy != "srnn":
-        bad.append("robot.policy=%r (only the srnn observation dict is produced)" % config.robot.policy)
+    if config.robot.policy not in ("srnn", "convgru"):
+        bad.append("robot.policy=%r (the srnn observation dict and the convgru LiDAR row are produced)"
+                   % config.robot.policy)
     if config.action_space.kinematics not in ("holonomic", "unicycle"):
         bad.append("action_space.kinematics=%r" % config.action_space.kinematics)
     if bad:

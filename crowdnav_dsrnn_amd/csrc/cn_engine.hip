@@ -2310,6 +2310,155 @@ __global__ void __launch_bounds__(256) cn_edge_features_kernel(int64_t E, int N,
 // ------------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------------
+// LiDAR observation of the ConvGRU policy: CrowdSimDict.generate_ob's 'convgru' branch
+// (crowd_sim_dict.py:96-101) over LidarSensor.sensor_spin (crowd_sim/envs/utils/lidarv2.py:398-427).
+// As shipped, the reference computes the scan only inside reset() (crowd_sim_dict.py:174-191, robot
+// heading atan2(0, 0) = 0, and only the LAST human is parsed: the append sits outside the loop), AFTER the
+// reset observation was built (:166), and step() never refreshes lidar_rel_dist. So the observation that
+// reset() returns carries the previous scan (zeros before the first), and every step of the episode
+// carries the scan taken at its reset. One 64-lane wave per env, three beams per lane, float64 as the
+// reference; the observation row is
+//   [clip(robot (px, py, r, gx, gy, v_pref, theta) / max_range, 0, 1), |1 - clip(dist / max_range, 0, 1)|].
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double np_rem(double a, double b)   // numpy float remainder (sign of divisor)
+{
+    double m = fmod(a, b);
+    if (m != 0.0) { if ((b < 0) != (m < 0)) m += b; }
+    else m = copysign(0.0, b);
+    return m;
+}
+__device__ __forceinline__ double rescale_angle(double t) { return np_rem(t + 2.0 * CN_PI, 2.0 * CN_PI); }
+
+__device__ __forceinline__ int seg_orient(double px, double py, double qx, double qy, double rx, double ry)
+{   // get_intersect.py:25-37
+    const double v = ((qy - py) * (rx - qx)) - ((qx - px) * (ry - qy));
+    return v > 0 ? 1 : (v < 0 ? 2 : 0);
+}
+__device__ __forceinline__ bool on_seg(double px, double py, double qx, double qy, double rx, double ry)
+{   // get_intersect.py:12-21
+    return qx <= fmax(px, rx) && qx >= fmin(px, rx) && qy <= fmax(py, ry) && qy >= fmin(py, ry);
+}
+
+__global__ void __launch_bounds__(256) cn_lidar_obs_kernel(cn_state_ptrs S, int E, int N, double half_world,
+                                                           const uint8_t *__restrict__ reset_mask, int enable,
+                                                           int beams, double max_range, double robot_r,
+                                                           float *__restrict__ lidar, float *__restrict__ obs)
+{
+    const int e = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (e >= E) return;
+    const int D = 7 + beams;
+    float *o = obs + (int64_t)e * D;
+    if (lane < 7) {
+        double v;
+        switch (lane) {
+        case 0: v = S.r_px[e]; break;
+        case 1: v = S.r_py[e]; break;
+        case 2: v = S.r_radius[e]; break;
+        case 3: v = S.r_gx[e]; break;
+        case 4: v = S.r_gy[e]; break;
+        case 5: v = S.r_vpref[e]; break;
+        default: v = S.r_theta[e]; break;
+        }
+        v = v / max_range;
+        v = v < 0.0 ? 0.0 : (v > 1.0 ? 1.0 : v);   // np.clip
+        o[lane] = (float)v;
+    }
+    float *L = lidar + (int64_t)e * beams;
+    const bool fresh = reset_mask == nullptr || reset_mask[e] != 0;
+    if (fresh) {
+        if (enable) {
+            const double sx = S.r_px[e], sy = S.r_py[e];
+            const int hl = e * N + (N - 1);                 // the last human only (see above)
+            const double hx = S.h_px[hl], hy = S.h_py[hl], hr = S.h_r[hl];
+            // get_valid_angles (lidarv2.py:17-52) for the one obstacle, sorted (min, max)
+            const double rlx = hx - sx, rly = hy - sy;
+            const double hd = rescale_angle(atan2(rly, rlx));
+            const double ddx = hr * sin(hd), ddy = hr * cos(hd);
+            const double m0 = rescale_angle(atan2(rly - ddy, rlx + ddx));
+            const double m1 = rescale_angle(atan2(rly + ddy, rlx - ddx));
+            const double lo0 = m0 < m1 ? m0 : m1, up0 = m0 < m1 ? m1 : m0;
+            const double bstep = (2.0 * CN_PI) / (double)(beams - 1);   // np.linspace(0, 2 pi, beams)
+            const int npts = 500;                                         // max_range / 0.01 samples (+ endpoint)
+            const double sstep = max_range / (double)(npts - 1);
+            for (int b = lane; b < beams; b += 64) {
+                const double th0 = (b == beams - 1) ? 2.0 * CN_PI : (double)b * bstep;
+                const double th = rescale_angle(th0 + 0.0);
+                // get_valid_angle_idx (lidarv2.py:55-75) mutates the caller's (min, max) arrays in place and
+                // they are reused for every beam: replay the mutation sequence up to this beam
+                double lo = lo0, up = up0, tt = th;
+                for (int q = 0; q <= b; ++q) {
+                    const bool wide = up - lo >= CN_PI;
+                    double tq = th;
+                    if (wide) { const double nu = up - 2.0 * CN_PI; up = lo; lo = nu; tq -= 2.0 * CN_PI; }
+                    if (q == b) tt = tq;
+                }
+                const bool valid = np_rem(tt - lo, 2.0 * CN_PI) < np_rem(up - lo, 2.0 * CN_PI);
+                const double c = cos(th), sn = sin(th);
+                double ex = c * max_range + sx, ey = sn * max_range + sy;   // beam_end
+                bool hit = false;
+                if (valid) {   // check_dist_collision_polygon (lidarv2.py:164-198): first sample inside the disc
+                    const double wx = hx - sx, wy = hy - sy;
+                    const double proj = wx * c + wy * sn, perp2 = wx * wx + wy * wy - proj * proj;
+                    const double r2 = hr * hr;
+                    if (perp2 <= r2 * (1.0 + 1e-9) + 1e-12) {
+                        const double hw = sqrt(fmax(r2 - perp2, 0.0));
+                        const double s_in = proj - hw, s_out = proj + hw;
+                        int k0 = (int)floor(s_in / sstep) - 2, k1 = (int)ceil(s_out / sstep) + 2;
+                        k0 = k0 < 0 ? 0 : k0;
+                        k1 = k1 > npts - 1 ? npts - 1 : k1;
+                        for (int k = k0; k <= k1 && !hit; ++k) {
+                            const double sk = (k == npts - 1) ? max_range : (double)k * sstep;
+                            const double bx = c * sk + sx, by = sn * sk + sy;
+                            const double ax = hx - bx, ay = hy - by;
+                            if (sqrt(ax * ax + ay * ay) < hr) { ex = bx; ey = by; hit = true; }
+                        }
+                    }
+                }
+                if (!hit) {    // walls (lidarv2.py:261-275): first intersecting wall, kept if within range
+                    const double t = half_world;
+                    const double wxs[5] = {-t, t, t, -t, -t}, wys[5] = {-t, -t, t, t, -t};
+                    const double p1x = sx, p1y = sy, q1x = ex, q1y = ey;
+                    for (int j = 0; j < 4; ++j) {
+                        const double p2x = wxs[j], p2y = wys[j], q2x = wxs[j + 1], q2y = wys[j + 1];
+                        const int o1 = seg_orient(p1x, p1y, q1x, q1y, p2x, p2y);
+                        const int o2 = seg_orient(p1x, p1y, q1x, q1y, q2x, q2y);
+                        const int o3 = seg_orient(p2x, p2y, q2x, q2y, p1x, p1y);
+                        const int o4 = seg_orient(p2x, p2y, q2x, q2y, q1x, q1y);
+                        const bool inter = (o1 != o2 && o3 != o4) || (o1 == 0 && on_seg(p1x, p1y, p2x, p2y, q1x, q1y)) ||
+                                           (o2 == 0 && on_seg(p1x, p1y, q2x, q2y, q1x, q1y)) ||
+                                           (o3 == 0 && on_seg(p2x, p2y, p1x, p1y, q2x, q2y)) ||
+                                           (o4 == 0 && on_seg(p2x, p2y, q1x, q1y, q2x, q2y));
+                        if (!inter) continue;
+                        // line_intersection (get_intersect.py:72-89)
+                        const double xd0 = p1x - q1x, xd1 = p2x - q2x, yd0 = p1y - q1y, yd1 = p2y - q2y;
+                        const double div = xd0 * yd1 - xd1 * yd0;
+                        if (div != 0.0) {
+                            const double d0 = p1x * q1y - p1y * q1x, d1 = p2x * q2y - p2y * q2x;
+                            const double ix = (d0 * xd1 - d1 * xd0) / div, iy = (d0 * yd1 - d1 * yd0) / div;
+                            if (np_norm2(ix - sx, iy - sy) <= max_range) { ex = ix; ey = iy; }
+                        }
+                        break;
+                    }
+                }
+                if (np_norm2(ex - sx, ey - sy) < robot_r) {   // beams cannot end inside the robot
+                    ex = sx + robot_r * cos(th);
+                    ey = sy + robot_r * sin(th);
+                }
+                const double rx = ex - sx, ry = ey - sy;
+                double rd = sqrt(rx * rx + ry * ry) / max_range;
+                rd = rd < 0.0 ? 0.0 : (rd > 1.0 ? 1.0 : rd);
+                o[7 + b] = L[b];                 // the reset observation keeps the previous scan
+                L[b] = (float)fabs(1.0 - rd);
+            }
+            return;
+        }
+        for (int b = lane; b < beams; b += 64) { o[7 + b] = L[b]; L[b] = 0.0f; }
+        return;
+    }
+    for (int b = lane; b < beams; b += 64) o[7 + b] = L[b];
+}
+
 struct cn_engine {
     cn_config c;
     int device;
@@ -2639,6 +2788,19 @@ int cn_debug_stamps(unsigned long long *a, unsigned long long *b)
     return CN_OK;
 }
 #endif
+
+int cn_lidar_obs(cn_engine *g, void *stream, const uint8_t *reset_mask, int enable, int beams, double max_range,
+                 double robot_radius, float *lidar, float *obs)
+{
+    if (!g) return set_err(CN_EINVAL, "null engine");
+    if (beams < 2 || beams > 4096 || !(max_range > 0) || !lidar || !obs)
+        return set_err(CN_EINVAL, "cn_lidar_obs: beams in [2, 4096], max_range > 0 and buffers required");
+    hipLaunchKernelGGL(cn_lidar_obs_kernel, dim3((unsigned)((g->E + 3) / 4)), dim3(256), 0, (hipStream_t)stream, g->s,
+                       g->E, g->N, 0.5 * g->c.square_width, reset_mask, enable, beams, max_range, robot_radius,
+                       lidar, obs);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
 
 int cn_edge_features(void *stream, int64_t E, int N, const float *robot_node, const float *temporal_edges,
                      const float *spatial_edges, const float *Wt, const float *bt, const float *Ws, const float *bs,

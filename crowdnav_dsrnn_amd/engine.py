@@ -78,6 +78,17 @@ class CrowdNavEngine:
         return self.obs(), self.reward, self.done, self.event, self.info, self.ep_return, self.ep_len
 
     # -------------------------------------------------------------------------------------------
+    def lidar_obs(self, out, lidar, reset_mask=None, enable=True, beams=180, max_range=5.0, robot_radius=0.3):
+        """The ConvGRU observation (cn_lidar_obs) into out (E,1,7+beams) f32; lidar (E,beams) f32 holds the
+        per-episode scans and is refreshed where reset_mask (E,) u8 is set (None = every env)."""
+        t = self.torch
+        with t.cuda.device(self.device):
+            _lib.check(_lib.lib().cn_lidar_obs(self._h, self._stream(),
+                                               None if reset_mask is None else reset_mask.data_ptr(),
+                                               int(bool(enable)), int(beams), float(max_range), float(robot_radius),
+                                               lidar.data_ptr(), out.data_ptr()))
+        return out
+
     def get_state(self):
         buf = np.zeros(self.state_bytes, np.uint8)
         with self.torch.cuda.device(self.device):

@@ -191,7 +191,18 @@ class CrowdNavVecEnv:
         if engine_device is None and self.device.type == "cuda":
             engine_device = self.device
         self.engine = CrowdNavEngine(self.cn_cfg, engine_device)
-        self.observation_space = spaces.observation_space(int(config.sim.human_num))
+        # 'convgru' observation (crowd_sim_dict.py:57-62, 96-101): robot state + the episode's LiDAR scan
+        self.obs_mode = "convgru" if getattr(config.robot, "policy", "srnn") == "convgru" else "srnn"
+        if self.obs_mode == "convgru":
+            lc = dict(config.lidar.cfg)
+            self._lidar_cfg = dict(enable=bool(config.lidar.enable), beams=int(lc["num_beams"]),
+                                   max_range=float(lc["max_range"]), robot_radius=float(lc["robot_radius"]))
+            B = self._lidar_cfg["beams"]
+            self.observation_space = spaces.lidar_observation_space(B)
+            self._lidar = torch.zeros((self.num_envs, B), dtype=torch.float32, device=self.engine.device)
+            self._lidar_obs = torch.zeros((self.num_envs, 1, 7 + B), dtype=torch.float32, device=self.engine.device)
+        else:
+            self.observation_space = spaces.observation_space(int(config.sim.human_num))
         self.action_space = spaces.action_space()
         self.scenario_names = list(abi.SCENARIOS)
         self.side_preference = bool(config.test.side_preference)
@@ -212,7 +223,12 @@ class CrowdNavVecEnv:
 
     # ---- VecEnv API --------------------------------------------------------------------------
     def _obs_out(self, o):
-        return {k: v.to(self.device, copy=True) for k, v in o.items()}
+        if isinstance(o, dict):
+            return {k: v.to(self.device, copy=True) for k, v in o.items()}
+        return o.to(self.device, copy=True)
+
+    def _convgru_obs(self, reset_mask):
+        return self.engine.lidar_obs(self._lidar_obs, self._lidar, reset_mask, **self._lidar_cfg)
 
     def reset(self):
         """VecPyTorch.reset (envs.py:215-222). Monitor forbids a second reset of a running episode
@@ -222,7 +238,10 @@ class CrowdNavVecEnv:
                                "wrap your env with Monitor(env, path, allow_early_resets=True)")
         self._was_reset = True
         self._state_cache = None
-        return self._obs_out(self.engine.reset())
+        o = self.engine.reset()
+        if self.obs_mode == "convgru":
+            o = self._convgru_obs(None)
+        return self._obs_out(o)
 
     def step_async(self, actions):
         self._pending = actions
@@ -258,7 +277,10 @@ class CrowdNavVecEnv:
         if not isinstance(actions, t.Tensor):
             actions = t.as_tensor(np.asarray(actions, dtype=np.float32))
         self._state_cache = None
-        return self.engine.step(actions.reshape(self.num_envs, 2))
+        out = self.engine.step(actions.reshape(self.num_envs, 2))
+        if self.obs_mode == "convgru":
+            out = (self._convgru_obs(out[2]),) + tuple(out[1:])
+        return out
 
     def _state(self):
         if self._state_cache is None:

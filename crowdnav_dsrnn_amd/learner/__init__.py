@@ -5,4 +5,4 @@ resident on the GPU; with torch.distributed initialised (one process per GPU, ba
 the gradients are all-reduced per minibatch and the advantage normalisation uses global statistics.
 """
 from .ppo import PPO  # noqa: F401
-from .storage import SRNNRolloutStorage  # noqa: F401
+from .storage import RolloutStorage, SRNNRolloutStorage  # noqa: F401

@@ -12,7 +12,7 @@ import time
 
 import torch
 
-from .storage import SRNNRolloutStorage
+from .storage import RolloutStorage, SRNNRolloutStorage
 
 
 class RolloutTrainer:
@@ -24,13 +24,21 @@ class RolloutTrainer:
         self.deterministic = deterministic
         dev = envs.engine.device
         self.device = dev
-        self.rollouts = SRNNRolloutStorage(config.ppo.num_steps, envs.num_envs, envs.observation_space.spaces,
-                                           envs.action_space, config.SRNN.human_node_rnn_size,
-                                           config.SRNN.human_human_edge_rnn_size, "GRU", device=dev,
-                                           compact_hidden=True)
+        if getattr(envs, "obs_mode", "srnn") == "convgru":   # train.py:157-172
+            self.rollouts = RolloutStorage(config.ppo.num_steps, envs.num_envs, envs.observation_space.shape,
+                                           envs.action_space, actor_critic.base.recurrent_hidden_state_size,
+                                           device=dev, compact_hidden=True)
+        else:
+            self.rollouts = SRNNRolloutStorage(config.ppo.num_steps, envs.num_envs, envs.observation_space.spaces,
+                                               envs.action_space, config.SRNN.human_node_rnn_size,
+                                               config.SRNN.human_human_edge_rnn_size, "GRU", device=dev,
+                                               compact_hidden=True)
         obs = envs.reset()
-        for k in self.rollouts.obs:
-            self.rollouts.obs[k][0].copy_(obs[k])
+        if isinstance(self.rollouts.obs, dict):
+            for k in self.rollouts.obs:
+                self.rollouts.obs[k][0].copy_(obs[k])
+        else:
+            self.rollouts.obs[0].copy_(obs)
         self.episode_returns = []
         self.env_steps = 0
 
@@ -40,7 +48,7 @@ class RolloutTrainer:
         ep_sum = torch.zeros((), dtype=torch.float64, device=self.device)
         ep_cnt = torch.zeros((), dtype=torch.int64, device=self.device)
         for step in range(r.num_steps):
-            obs_s = {k: v[step] for k, v in r.obs.items()}
+            obs_s = {k: v[step] for k, v in r.obs.items()} if isinstance(r.obs, dict) else r.obs[step]
             hxs_s = r.hidden(step)
             value, action, logp, hxs = self.ac.act(obs_s, hxs_s, r.masks[step], deterministic=self.deterministic)
             obs, reward, done, _, _, ep_ret, _ = self.envs.step_device(action)
@@ -57,7 +65,8 @@ class RolloutTrainer:
         ep_sum, ep_cnt = self.collect()
         r = self.rollouts
         with torch.no_grad():
-            next_value = self.ac.get_value({k: v[-1] for k, v in r.obs.items()},
+            last = {k: v[-1] for k, v in r.obs.items()} if isinstance(r.obs, dict) else r.obs[-1]
+            next_value = self.ac.get_value(last,
                                            r.hidden(r.num_steps),
                                            r.masks[-1]).detach()
         c = self.config

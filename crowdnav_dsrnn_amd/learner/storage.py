@@ -138,3 +138,94 @@ class SRNNRolloutStorage:
                    self.value_preds[:-1].reshape(-1, 1)[idx], self.returns[:-1].reshape(-1, 1)[idx],
                    self.masks[:-1].reshape(-1, 1)[idx], self.action_log_probs.reshape(-1, 1)[idx],
                    None if advantages is None else advantages.reshape(-1, 1)[idx])
+
+
+class RolloutStorage(SRNNRolloutStorage):
+    """RolloutStorage (pytorchBaselines/a2c_ppo_acktr/storage.py:295-508): the buffer train.py uses for the
+    ConvGRU policy (train.py:157-172) — one observation tensor and one (E, H) recurrent state instead of the
+    DSRNN's dicts. Returns, after_update and both generators follow the reference; compact_hidden as in
+    SRNNRolloutStorage."""
+
+    def __init__(self, num_steps, num_processes, obs_shape, action_space, recurrent_hidden_state_size, device=None,
+                 compact_hidden=False):
+        T, E = num_steps, num_processes
+        dev = device
+        self.compact_hidden = bool(compact_hidden)
+        TH = 2 if compact_hidden else T + 1
+        self.obs = torch.zeros(T + 1, E, *tuple(obs_shape), device=dev)
+        self.recurrent_hidden_states = torch.zeros(TH, E, recurrent_hidden_state_size, device=dev)
+        self.rewards = torch.zeros(T, E, 1, device=dev)
+        self.value_preds = torch.zeros(T + 1, E, 1, device=dev)
+        self.returns = torch.zeros(T + 1, E, 1, device=dev)
+        self.action_log_probs = torch.zeros(T, E, 1, device=dev)
+        if action_space.__class__.__name__ == "Discrete":
+            raise NotImplementedError("CrowdSimDict has a Box(2,) action space")
+        self.actions = torch.zeros(T, E, action_space.shape[0], device=dev)
+        self.masks = torch.ones(T + 1, E, 1, device=dev)
+        self.bad_masks = torch.ones(T + 1, E, 1, device=dev)
+        self.num_steps = T
+        self.step = 0
+
+    def to(self, device):
+        for n in ("obs", "recurrent_hidden_states", "rewards", "value_preds", "returns", "action_log_probs",
+                  "actions", "masks", "bad_masks"):
+            setattr(self, n, getattr(self, n).to(device))
+        return self
+
+    def insert(self, obs, recurrent_hidden_states, actions, action_log_probs, value_preds, rewards, masks,
+               bad_masks):
+        s = self.step
+        self.obs[s + 1].copy_(obs)
+        self.recurrent_hidden_states[1 if self.compact_hidden else s + 1].copy_(recurrent_hidden_states)
+        self.actions[s].copy_(actions)
+        self.action_log_probs[s].copy_(action_log_probs)
+        self.value_preds[s].copy_(value_preds)
+        self.rewards[s].copy_(rewards)
+        self.masks[s + 1].copy_(masks)
+        self.bad_masks[s + 1].copy_(bad_masks)
+        self.step = (s + 1) % self.num_steps
+
+    def hidden(self, step):
+        return self.recurrent_hidden_states[(0 if step == 0 else 1) if self.compact_hidden else step]
+
+    def after_update(self):
+        self.obs[0].copy_(self.obs[-1])
+        self.recurrent_hidden_states[0].copy_(self.recurrent_hidden_states[-1])
+        self.masks[0].copy_(self.masks[-1])
+        self.bad_masks[0].copy_(self.bad_masks[-1])
+
+    def recurrent_generator(self, advantages, num_mini_batch):
+        """storage.py:449-508 (same torch.randperm draw as the reference)."""
+        E = self.rewards.size(1)
+        assert E >= num_mini_batch, "PPO requires num_processes >= num_mini_batch"
+        n = E // num_mini_batch
+        perm = torch.randperm(E)
+        T = self.num_steps
+        for start in range(0, E, n):
+            ind = perm[start:start + n].to(self.rewards.device)
+            yield (_flatten_helper(T, n, self.obs[:-1].index_select(1, ind)),
+                   self.recurrent_hidden_states[0].index_select(0, ind),
+                   _flatten_helper(T, n, self.actions.index_select(1, ind)),
+                   _flatten_helper(T, n, self.value_preds[:-1].index_select(1, ind)),
+                   _flatten_helper(T, n, self.returns[:-1].index_select(1, ind)),
+                   _flatten_helper(T, n, self.masks[:-1].index_select(1, ind)),
+                   _flatten_helper(T, n, self.action_log_probs.index_select(1, ind)),
+                   _flatten_helper(T, n, advantages.index_select(1, ind)))
+
+    def feed_forward_generator(self, advantages, num_mini_batch=None, mini_batch_size=None):
+        """storage.py:408-447."""
+        from torch.utils.data.sampler import BatchSampler, SubsetRandomSampler
+
+        T, E = self.rewards.shape[0:2]
+        batch = T * E
+        if mini_batch_size is None:
+            assert batch >= num_mini_batch
+            mini_batch_size = batch // num_mini_batch
+        for indices in BatchSampler(SubsetRandomSampler(range(batch)), mini_batch_size, drop_last=True):
+            idx = torch.as_tensor(indices, device=self.rewards.device)
+            yield (self.obs[:-1].reshape(-1, *self.obs.shape[2:])[idx],
+                   self.recurrent_hidden_states[:-1].reshape(-1, self.recurrent_hidden_states.shape[-1])[idx],
+                   self.actions.reshape(-1, self.actions.shape[-1])[idx], self.value_preds[:-1].reshape(-1, 1)[idx],
+                   self.returns[:-1].reshape(-1, 1)[idx], self.masks[:-1].reshape(-1, 1)[idx],
+                   self.action_log_probs.reshape(-1, 1)[idx],
+                   None if advantages is None else advantages.reshape(-1, 1)[idx])

@@ -1,4 +1,4 @@
-"""Policy wrapper (pytorchBaselines/a2c_ppo_acktr/model.py:17-104): base='srnn' + DiagGaussian.
+"""Policy wrapper (pytorchBaselines/a2c_ppo_acktr/model.py:17-104): base='srnn' or 'convgru' + DiagGaussian.
 
 API and return values as in the reference:
   act(inputs, rnn_hxs, masks, deterministic=False) -> value (E,1), action (E,2), log_prob (E,1), rnn_hxs
@@ -8,6 +8,7 @@ API and return values as in the reference:
 """
 import torch.nn as nn
 
+from .convgru_model import ConvGRU
 from .distributions import DiagGaussian
 from .srnn_model import SRNN
 
@@ -15,13 +16,19 @@ from .srnn_model import SRNN
 class Policy(nn.Module):
     def __init__(self, obs_shape, action_space, base=None, base_kwargs=None):
         super().__init__()
-        if base != "srnn":
-            raise NotImplementedError("only base='srnn' is provided (the ConvGRU/LiDAR policy is out of scope)")
-        self.base = SRNN(obs_shape, base_kwargs)
-        self.srnn = True
+        if base == "srnn":
+            self.base = SRNN(obs_shape, base_kwargs)
+            self.srnn, self.convgru = True, False
+            dist_in = self.base.output_size
+        elif base == "convgru":   # model.py:25-33: the LiDAR policy; its distribution reads actor.fc2 (64)
+            self.base = ConvGRU(obs_shape, base_kwargs)
+            self.srnn, self.convgru = False, True
+            dist_in = self.base.actor.fc2.out_features
+        else:
+            raise NotImplementedError("base must be 'srnn' or 'convgru'")
         if action_space.__class__.__name__ != "Box":
-            raise NotImplementedError("DSRNN drives a Box(2,) action space")
-        self.dist = DiagGaussian(self.base.output_size, action_space.shape[0])
+            raise NotImplementedError("CrowdSimDict drives a Box(2,) action space")
+        self.dist = DiagGaussian(dist_in, action_space.shape[0])
 
     @property
     def is_recurrent(self):
@@ -30,15 +37,20 @@ class Policy(nn.Module):
     def forward(self, inputs, rnn_hxs, masks):
         raise NotImplementedError
 
+    def _infer(self, inputs, rnn_hxs, masks):
+        if self.srnn:
+            return self.base(inputs, rnn_hxs, masks, infer=True)
+        return self.base(inputs, rnn_hxs, masks)
+
     def act(self, inputs, rnn_hxs, masks, deterministic=False):
-        value, actor_features, rnn_hxs = self.base(inputs, rnn_hxs, masks, infer=True)
+        value, actor_features, rnn_hxs = self._infer(inputs, rnn_hxs, masks)
         dist = self.dist(actor_features)
         action = dist.mode() if deterministic else dist.sample()
         action_log_probs = dist.log_probs(action)
         return value, action, action_log_probs, rnn_hxs
 
     def get_value(self, inputs, rnn_hxs, masks):
-        value, _, _ = self.base(inputs, rnn_hxs, masks, infer=True)
+        value, _, _ = self._infer(inputs, rnn_hxs, masks)
         return value
 
     def evaluate_actions(self, inputs, rnn_hxs, masks, action):

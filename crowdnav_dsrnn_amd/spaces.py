@@ -56,6 +56,11 @@ def observation_space(human_num):
     return _GymDict(d) if _GymDict is not None else Dict(d)
 
 
+def lidar_observation_space(num_beams):
+    """The ConvGRU policy's observation: Box (1, 7 + num_beams) float32 (crowd_sim_dict.py:57-62)."""
+    return _box((1, 7 + int(num_beams)))
+
+
 def action_space():
     """Box(2,) float32, unbounded (crowd_sim_dict.py:64-69)."""
     return _box((2,))

@@ -22,6 +22,8 @@
  *   cn_gru_fwd_step / cn_gru_bwd_step ⟵ one time step of the mask-segmented GRU
  *                   (srnn_model.py:52-104 RNNBase._forward_gru, torch nn.GRU cell math) and its gradient;
  *                   the GEMMs around them (x W_ih^T, hm W_hh^T, dgh W_hh) are library GEMMs
+ *   cn_lidar_obs     ⟵ CrowdSimDict.generate_ob's 'convgru' observation (crowd_sim_dict.py:96-101) with
+ *                   LidarSensor.sensor_spin (crowd_sim/envs/utils/lidarv2.py:398-427) evaluated at reset
  *   cn_attn_pool_fwd / cn_attn_pool_bwd ⟵ EdgeAttention's weighted sum of the spatial edge states
  *                   (srnn_model.py:320-333, torch.bmm(h_spatials^T, attn)) and its gradient
  *
@@ -197,6 +199,18 @@ int cn_gru_fwd_step(void *stream, int64_t B, int H, const float *gi, const float
  * acc <- dL/dh_t * z (the caller then adds dgh W_hh to obtain dL/dhm_t). */
 int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
                     const float *save, const float *hm, float *dgi, float *dgh);
+
+/* The ConvGRU observation row of every env, obs [E][7 + beams] float32:
+ *   [clip(robot (px, py, radius, gx, gy, v_pref, theta) / max_range, 0, 1), scan].
+ * lidar [E][beams] (caller-owned, zero-initialised) holds each env's current scan
+ * |1 - clip(dist / max_range, 0, 1)|. For envs with reset_mask[e] != 0 (NULL = all envs, i.e. after
+ * cn_reset; pass the `done` output of cn_step after a step) the observation carries the scan held so far
+ * and the scan is then retaken from the engine state — the reference builds reset()'s observation before
+ * it spins the sensor (crowd_sim_dict.py:166-191), at robot heading 0, against the last human and the
+ * world walls. Other envs get the held scan. enable = 0: scans stay zero (config.lidar.enable False).
+ * Call after cn_reset / cn_step on the same stream. */
+int cn_lidar_obs(cn_engine *eng, void *stream, const uint8_t *reset_mask, int enable, int beams, double max_range,
+                 double robot_radius, float *lidar, float *obs);
 
 /* out[r][h] = sum_n hs[r][n][h] * attn[r][n]; hs [R][N][H], attn [R][N], out [R][H]; H % 4 == 0. */
 int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, float *out);

@@ -14,6 +14,9 @@ oracle/shims (gym, shapely, rvo2, torchvision — see oracle/shims/README.md) an
                  (pytorchBaselines/a2c_ppo_acktr/model.py:63-104, srnn_model.py:409-504)
   eval_*.npz     pytorchBaselines/evaluation.py evaluate() + metrics.py Metrics driven by a scripted
                  episode stream (stand-in VecEnv / policy objects; the bookkeeping is the reference's)
+  lidar_*.npz    CrowdSimDict.reset() with robot.policy = 'convgru' and lidar.enable: post-reset states and
+                 the (1, 7 + 180) observation (crowd_sim_dict.py:96-101,170-191; lidarv2.py)
+  convgru.npz    ConvGRU Policy.act / evaluate_actions with procedural weights (convgru_model.py, model.py)
   ppo.npz        SRNNRolloutStorage + compute_returns + PPO.update on procedural weights
                  (pytorchBaselines/a2c_ppo_acktr/storage.py:14-292, algo/ppo.py:36-118)
 
@@ -22,7 +25,8 @@ copied. The reference never travels to the GPU box; these .npz files do.
 Deviations applied to the reference while recording (each documented in DESIGN.md):
   - unicycle: ActionRot gets vx/vy = commanded world-frame velocity so calc_reward's jerk/speed
     metrics do not raise (crowd_sim.py:1004 reads action.vx; SURVEY §9-1);
-  - the ORCA frozen-simulator parameters are read back from the rvo2 shim into the state.
+  - the ORCA frozen-simulator parameters are read back from the rvo2 shim into the state;
+  - LiDAR: `np.int` (removed in NumPy 1.24, used at lidarv2.py:251) is aliased to `int` while recording.
 """
 import argparse
 import math
@@ -529,6 +533,120 @@ def gen_ppo(outdir):
     print("ppo ok")
 
 
+def gen_lidar(name, cfg, E, resets, outdir):
+    """Post-reset states + ConvGRU observations of the reference (LiDAR scan at reset)."""
+    if not hasattr(np, "int"):
+        np.int = int   # lidarv2.py:251 (np.int was removed in NumPy 1.24)
+    cfg.robot.policy = "convgru"
+    cfg.lidar.enable = True
+    envs = [make_ref_env(cfg, r, E) for r in range(E)]
+    out = {"meta_" + k: np.array(v) for k, v in cfg_meta(cfg, E).items()}
+    out["meta_max_range"] = np.array(float(cfg.lidar.cfg["max_range"]))
+    out["meta_num_beams"] = np.array(int(cfg.lidar.cfg["num_beams"]))
+    out["meta_lidar_robot_radius"] = np.array(float(cfg.lidar.cfg["robot_radius"]))
+    for k in range(resets):
+        obs = [np.asarray(env_reset(env), np.float32).reshape(1, -1) for env in envs]
+        pack_state(extract(envs, cfg), "k%d_post_" % k, out, True)
+        out["k%d_obs" % k] = np.stack(obs)
+    out["resets"] = np.array(resets)
+    np.savez_compressed(os.path.join(outdir, "lidar_%s.npz" % name), **out)
+    print("lidar", name, "ok")
+
+
+def gen_convgru(outdir):
+    """ConvGRU policy (pytorchBaselines/a2c_ppo_acktr/convgru_model.py + model.py) on procedural weights:
+    act (one step, E envs) and evaluate_actions (T steps x E envs, episode starts inside)."""
+    import torch
+
+    torch.set_num_threads(4)
+    import gym
+    from pytorchBaselines.a2c_ppo_acktr.model import Policy
+
+    E, T, B = 5, 4, 180
+    cfg = make_ref_config(N=5)
+    cfg.robot.policy = "convgru"
+    obs_space = gym.spaces.Box(-np.inf, np.inf, (1, 7 + B))
+    act_space = gym.spaces.Box(-np.inf, np.inf, (2,))
+    torch.manual_seed(0)
+    pol = Policy(obs_space, act_space, base="convgru", base_kwargs=cfg)
+    pol.load_state_dict(procedural_state_dict(pol))
+    pol.srnn = False
+    rng = np.random.RandomState(17)
+    out = {"state_dict_keys": np.array(sorted(pol.state_dict().keys()))}
+    obs = rng.uniform(0, 1, (E, 1, 7 + B)).astype(np.float32)
+    hxs = (rng.normal(0, 0.5, (E, 256))).astype(np.float32)
+    masks = np.array([[1.0], [0.0], [1.0], [1.0], [0.0]], np.float32)
+    with torch.no_grad():
+        v, a, lp, h = pol.act(torch.from_numpy(obs), torch.from_numpy(hxs), torch.from_numpy(masks), deterministic=True)
+    out.update(act_obs=obs, act_hxs=hxs, act_masks=masks, act_value=v.numpy(), act_action=a.numpy(),
+               act_logp=lp.numpy(), act_hxs_out=h.numpy())
+    obs_t = rng.uniform(0, 1, (T * E, 1, 7 + B)).astype(np.float32)
+    m_t = np.ones((T * E, 1), np.float32)
+    m_t[[0, 7, 13]] = 0.0
+    acts = rng.normal(0, 1, (T * E, 2)).astype(np.float32)
+    v, lp, ent, h = pol.evaluate_actions(torch.from_numpy(obs_t), torch.from_numpy(hxs), torch.from_numpy(m_t),
+                                         torch.from_numpy(acts))
+    out.update(ev_obs=obs_t, ev_masks=m_t, ev_actions=acts, ev_value=v.detach().numpy(),
+               ev_logp=lp.detach().numpy(), ev_entropy=np.float32(ent.item()), ev_hxs_out=h.detach().numpy())
+    np.savez_compressed(os.path.join(outdir, "convgru.npz"), **out)
+    print("convgru ok")
+
+
+def gen_rollout_storage(outdir):
+    """RolloutStorage (storage.py:295-508, the ConvGRU buffer): inserts, the four compute_returns branches
+    and the recurrent / feed-forward minibatches for seeded torch permutations."""
+    import torch
+
+    import gym
+    from pytorchBaselines.a2c_ppo_acktr.storage import RolloutStorage
+
+    T, E, D, H = 6, 4, 10, 8
+    rng = np.random.RandomState(23)
+    out = {}
+    r = lambda *s: rng.normal(0, 1, s).astype(np.float32)  # noqa: E731
+    seq = {"obs0": r(E, 1, D)}
+    for t in range(T):
+        seq["t%d" % t] = dict(obs=r(E, 1, D), hxs=r(E, H), act=r(E, 2), logp=r(E, 1), val=r(E, 1), rew=r(E, 1),
+                             masks=(rng.rand(E, 1) > 0.3).astype(np.float32),
+                             bad=(rng.rand(E, 1) > 0.2).astype(np.float32))
+    nv = r(E, 1)
+    out["obs0"] = seq["obs0"]
+    out["next_value"] = nv
+    for t in range(T):
+        for k, v in seq["t%d" % t].items():
+            out["t%d_%s" % (t, k)] = v
+
+    def filled():
+        st = RolloutStorage(T, E, (1, D), gym.spaces.Box(-np.inf, np.inf, (2,)), H)
+        st.obs[0].copy_(torch.from_numpy(seq["obs0"]))
+        for t in range(T):
+            g = seq["t%d" % t]
+            st.insert(*[torch.from_numpy(g[k]) for k in ("obs", "hxs", "act", "logp", "val", "rew", "masks", "bad")])
+        return st
+
+    for gae in (True, False):
+        for ptl in (True, False):
+            st = filled()
+            st.compute_returns(torch.from_numpy(nv), gae, 0.99, 0.95, ptl)
+            out["returns_%d%d" % (gae, ptl)] = st.returns.numpy().copy()
+    st = filled()
+    adv = torch.from_numpy(r(T, E, 1))
+    out["adv"] = adv.numpy()
+    torch.manual_seed(5)
+    for i, b in enumerate(st.recurrent_generator(adv, 2)):
+        for j, x in enumerate(b):
+            out["rec%d_%d" % (i, j)] = x.numpy().copy()
+    torch.manual_seed(6)
+    for i, b in enumerate(st.feed_forward_generator(adv, 3)):
+        for j, x in enumerate(b):
+            out["ff%d_%d" % (i, j)] = x.numpy().copy()
+    st.after_update()
+    out["after_obs0"] = st.obs[0].numpy().copy()
+    out["after_hxs0"] = st.recurrent_hidden_states[0].numpy().copy()
+    np.savez_compressed(os.path.join(outdir, "rollout_storage.npz"), **out)
+    print("rollout_storage ok")
+
+
 EVAL_SCEN = ("circle_crossing", "square_crossing", "parallel_traffic")
 
 
@@ -756,6 +874,21 @@ def main():
         gen_ppo(args.out)
     if want("eval"):
         gen_eval(args.out)
+    def _radius(c, r):
+        c.sim.circle_radius = r
+        return c
+
+    lidar_cases = [("circle_N5_r7", _radius(make_ref_config(N=5), 7.0), 16, 3),
+                   ("circle_N10_r6", _radius(make_ref_config(N=10), 6.0), 16, 3),
+                   ("square_N8_unicycle", make_ref_config(kin="unicycle", N=8, scenarios=("square_crossing",)), 12, 3),
+                   ("circle_N1_r8", _radius(make_ref_config(N=1), 8.0), 16, 4)]
+    for name, cfg, E, R in lidar_cases:
+        if want("lidar_" + name):
+            gen_lidar(name, cfg, E, R, args.out)
+    if want("convgru"):
+        gen_convgru(args.out)
+    if want("rollout_storage"):
+        gen_rollout_storage(args.out)
 
 
 if __name__ == "__main__":

@@ -74,9 +74,13 @@ def test_make_cn_config_rejects_unsupported_reference_options():
     with pytest.raises(UnsupportedConfig):
         make_cn_config(c, 4)
     c = clone_config(Config())
-    c.lidar.enable = True
+    c.robot.policy = "cadrl"
     with pytest.raises(UnsupportedConfig):
         make_cn_config(c, 4)
+    c = clone_config(Config())        # the LiDAR / ConvGRU observation is served (cn_lidar_obs)
+    c.lidar.enable = True
+    c.robot.policy = "convgru"
+    make_cn_config(c, 4)
 
 
 def test_make_cn_config_defaults_follow_make_env():

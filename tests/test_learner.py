@@ -177,3 +177,42 @@ def test_ppo_data_parallel_gloo(tmp_path):
     mean, std = raw.mean(), raw.std()
     np.testing.assert_allclose(r0["adv"].numpy(), ((r0["raw"].double() - mean) / (std + 1e-5)).numpy(), atol=1e-5)
     np.testing.assert_allclose(r1["adv"].numpy(), ((r1["raw"].double() - mean) / (std + 1e-5)).numpy(), atol=1e-5)
+
+
+def _rollout_storage(z, compact=False):
+    from crowdnav_dsrnn_amd.learner import RolloutStorage
+
+    T, E = 6, 4
+    st = RolloutStorage(T, E, (1, 10), Box(-np.inf, np.inf, (2,)), 8, compact_hidden=compact)
+    st.obs[0].copy_(torch.from_numpy(z["obs0"]))
+    for t in range(T):
+        st.insert(*[torch.from_numpy(z["t%d_%s" % (t, k)]) for k in ("obs", "hxs", "act", "logp", "val", "rew",
+                                                                      "masks", "bad")])
+    return st
+
+
+def test_rollout_storage_vs_reference():
+    """RolloutStorage (storage.py:295-508, the ConvGRU buffer) vs tests/golden/rollout_storage.npz."""
+    z = load("rollout_storage.npz")
+    for gae in (True, False):
+        for ptl in (True, False):
+            st = _rollout_storage(z)
+            st.compute_returns(torch.from_numpy(z["next_value"]), gae, 0.99, 0.95, ptl)
+            want = z["returns_%d%d" % (gae, ptl)]
+            sl = slice(None) if not gae else slice(0, -1)   # returns[-1] is written by the non-GAE branches only
+            np.testing.assert_allclose(st.returns.numpy()[sl], want[sl], atol=1e-6, rtol=0)
+    for compact in (False, True):
+        st = _rollout_storage(z, compact)
+        adv = torch.from_numpy(z["adv"])
+        torch.manual_seed(5)
+        for i, b in enumerate(st.recurrent_generator(adv, 2)):
+            for j, x in enumerate(b):
+                np.testing.assert_array_equal(x.numpy(), z["rec%d_%d" % (i, j)], err_msg="rec %d %d" % (i, j))
+        if not compact:
+            torch.manual_seed(6)
+            for i, b in enumerate(st.feed_forward_generator(adv, 3)):
+                for j, x in enumerate(b):
+                    np.testing.assert_array_equal(x.numpy(), z["ff%d_%d" % (i, j)], err_msg="ff %d %d" % (i, j))
+        st.after_update()
+        np.testing.assert_array_equal(st.obs[0].numpy(), z["after_obs0"])
+        np.testing.assert_array_equal(st.recurrent_hidden_states[0].numpy(), z["after_hxs0"])
