@@ -2481,7 +2481,7 @@ struct cn_engine {
     uint64_t nstep;
     // kernel timing (cn_profile)
     int prof_on, prof_cap, prof_n;
-    hipEvent_t *ev;  // [3 * prof_cap]: before A, after A, after B
+    hipEvent_t *ev;  // [2]: before the first, after the last launch of the window
 };
 
 static thread_local char g_err[512];
@@ -2588,13 +2588,15 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     hipError_t e4 = hipMalloc(&g->plist, sizeof(uint32_t) * 3 * (g->E + 64));
     hipError_t e5 = hipMalloc(&g->pend_mem, pend_bytes);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
-        hipFree(g->state); hipFree(g->work); hipFree(g->work_count); hipFree(g->plist); hipFree(g->pend_mem);
+        (void)hipFree(g->state); (void)hipFree(g->work); (void)hipFree(g->work_count); (void)hipFree(g->plist); (void)hipFree(g->pend_mem);
         delete g;
         return set_err(CN_ENOMEM, "hipMalloc failed");
     }
-    hipMemset(g->state, 0, g->state_bytes);
-    hipMemset(g->work_count, 0, 64);
-    hipMemset(g->pend_mem, 0, pend_bytes);
+    if (hipMemset(g->state, 0, g->state_bytes) != hipSuccess || hipMemset(g->work_count, 0, 64) != hipSuccess ||
+        hipMemset(g->pend_mem, 0, pend_bytes) != hipSuccess) {
+        cn_destroy(g);
+        return set_err(CN_EHIP, "hipMemset failed");
+    }
     {
         char *b = (char *)g->pend_mem;
         g->pend.mt = (uint32_t *)b; b += pb_mt;
@@ -2623,8 +2625,11 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     // unit-circle table of GEOS's 64-gon point buffer (norm zones)
     double cs[64], sn[64];
     for (int k = 0; k < 64; ++k) { const double a = -(k * (CN_PI / 2 / 16)); cs[k] = cos(a); sn[k] = sin(a); }
-    hipMemcpyToSymbol(HIP_SYMBOL(c_circ_cos), cs, sizeof cs);
-    hipMemcpyToSymbol(HIP_SYMBOL(c_circ_sin), sn, sizeof sn);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_circ_cos), cs, sizeof cs) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(c_circ_sin), sn, sizeof sn) != hipSuccess) {
+        cn_destroy(g);
+        return set_err(CN_EHIP, "hipMemcpyToSymbol failed");
+    }
     if (g->a_lds > 160 * 1024) { cn_destroy(g); return set_err(CN_EUNSUPPORTED, "LDS plan exceeds 160 KiB"); }
     if (g->a_lds > 64 * 1024) {
         (void)hipFuncSetAttribute((const void *)cn_step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2641,21 +2646,24 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
 static void prof_free(cn_engine *g)
 {
     if (g->ev) {
-        for (int k = 0; k < 3 * g->prof_cap; ++k) (void)hipEventDestroy(g->ev[k]);
+        for (int k = 0; k < 2; ++k) (void)hipEventDestroy(g->ev[k]);
         delete[] g->ev;
     }
     g->ev = nullptr;
     g->prof_cap = g->prof_n = g->prof_on = 0;
 }
 
+// Two events bracket the whole window of `max_steps` launches (one before the first, one after the
+// last): per-launch event pairs cost ~12 us of stream time each on this GPU, more than the launch gaps
+// they would exclude (back-to-back step launches are separated by < 0.2 us).
 int cn_profile(cn_engine *g, int enable, int max_steps)
 {
     if (!g) return set_err(CN_EINVAL, "null engine");
     prof_free(g);
     if (!enable) return CN_OK;
     if (max_steps <= 0) return set_err(CN_EINVAL, "max_steps must be > 0");
-    g->ev = new hipEvent_t[3 * max_steps];
-    for (int k = 0; k < 3 * max_steps; ++k) HIPCHK(hipEventCreate(&g->ev[k]));
+    g->ev = new hipEvent_t[2];
+    for (int k = 0; k < 2; ++k) HIPCHK(hipEventCreate(&g->ev[k]));
     g->prof_cap = max_steps;
     g->prof_on = 1;
     return CN_OK;
@@ -2664,16 +2672,14 @@ int cn_profile(cn_engine *g, int enable, int max_steps)
 int cn_profile_read(cn_engine *g, double *a_ms, double *b_ms, int64_t *launches)
 {
     if (!g) return set_err(CN_EINVAL, "null engine");
-    double sa = 0, sb = 0;
-    if (g->prof_n > 0) HIPCHK(hipEventSynchronize(g->ev[3 * (g->prof_n - 1) + 2]));
-    for (int k = 0; k < g->prof_n; ++k) {
-        float ta = 0, tb = 0;
-        HIPCHK(hipEventElapsedTime(&ta, g->ev[3 * k], g->ev[3 * k + 1]));
-        HIPCHK(hipEventElapsedTime(&tb, g->ev[3 * k + 1], g->ev[3 * k + 2]));
-        sa += ta; sb += tb;
+    float ta = 0;
+    if (g->prof_n > 0) {
+        if (g->prof_n < g->prof_cap) return set_err(CN_EINVAL, "profile window not complete (fewer launches than max_steps)");
+        HIPCHK(hipEventSynchronize(g->ev[1]));
+        HIPCHK(hipEventElapsedTime(&ta, g->ev[0], g->ev[1]));
     }
-    if (a_ms) *a_ms = sa;
-    if (b_ms) *b_ms = sb;
+    if (a_ms) *a_ms = ta;
+    if (b_ms) *b_ms = 0;
     if (launches) *launches = g->prof_n;
     return CN_OK;
 }
@@ -2681,13 +2687,13 @@ int cn_profile_read(cn_engine *g, double *a_ms, double *b_ms, int64_t *launches)
 void cn_destroy(cn_engine *g)
 {
     if (!g) return;
-    hipSetDevice(g->device);
+    (void)hipSetDevice(g->device);
     prof_free(g);
-    hipFree(g->state);
-    hipFree(g->work);
-    hipFree(g->work_count);
-    hipFree(g->plist);
-    hipFree(g->pend_mem);
+    (void)hipFree(g->state);
+    (void)hipFree(g->work);
+    (void)hipFree(g->work_count);
+    (void)hipFree(g->plist);
+    (void)hipFree(g->pend_mem);
     delete g;
 }
 
@@ -2714,7 +2720,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     const int kw = (int)(g->nstep % 3), kr = (int)((g->nstep + 2) % 3), kz = (int)((g->nstep + 1) % 3);
     ++g->nstep;
     const bool prof = g->prof_on && g->prof_n < g->prof_cap;
-    if (prof) HIPCHK(hipEventRecord(g->ev[3 * g->prof_n], st));
+    if (prof && g->prof_n == 0) HIPCHK(hipEventRecord(g->ev[0], st));
     StepArgs a;
     a.s = g->s; a.actions = actions; a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
     a.reward = reward; a.done = done; a.event = event; a.info = info; a.ep_return = ep_return; a.ep_len = ep_len;
@@ -2735,11 +2741,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     else
         hipLaunchKernelGGL(cn_step_kernel<false>, dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
     HIPCHK(hipGetLastError());
-    if (prof) {
-        HIPCHK(hipEventRecord(g->ev[3 * g->prof_n + 1], st));
-        HIPCHK(hipEventRecord(g->ev[3 * g->prof_n + 2], st));
-        ++g->prof_n;
-    }
+    if (prof && ++g->prof_n == g->prof_cap) HIPCHK(hipEventRecord(g->ev[1], st));
     return CN_OK;
 }
 

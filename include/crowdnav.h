@@ -166,9 +166,12 @@ int cn_get_state(cn_engine *eng, void *stream, void *dst, int dst_on_host);
 int cn_set_state(cn_engine *eng, void *stream, const void *src, int src_on_host);
 const void *cn_state_device_ptr(const cn_engine *eng);
 
-/* Kernel timing (measurement hook for bench.py's roofline): while enabled, cn_step records HIP events
- * on its stream around the step kernel (A) and the RNG/auto-reset kernel (B) for up to `max_steps`
- * calls. cn_profile_read synchronises on the last event and returns the summed kernel times. */
+/* Kernel timing (measurement hook for bench.py's roofline): while enabled, cn_step records one HIP event
+ * on its stream before the first and one after the `max_steps`-th step launch of the window (per-launch
+ * event pairs would cost ~12 us of stream time per step). cn_profile_read synchronises on the closing
+ * event and returns the window's span in step_kernel_ms (back-to-back launches: the summed launch
+ * durations) and the launch count; rng_kernel_ms is always 0 (the RNG work is fused into the step
+ * kernel). Reading an incomplete window is CN_EINVAL. */
 int cn_profile(cn_engine *eng, int enable, int max_steps);
 int cn_profile_read(cn_engine *eng, double *step_kernel_ms, double *rng_kernel_ms, int64_t *launches);
 
