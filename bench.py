@@ -46,7 +46,7 @@ def algorithmic_bytes_per_env_step(N):
     return 2 * (112 + 96 * N) + 8 + 4 * (9 + 2 * N) + 4 + 2
 
 
-def make_config(E, N, env_offset, nenv, workload="c2"):
+def make_config(E, N, env_offset, nenv, workload="c2", rng="mt19937"):
     """SURVEY.md §8d workloads. c2 (default, the BASELINE metric): circle_crossing, ORCA, unicycle.
     c3: square_crossing ("random crossing"), robot/human FOV = pi, holonomic. c5 is two engines
     (see engines_for)."""
@@ -62,10 +62,10 @@ def make_config(E, N, env_offset, nenv, workload="c2"):
     else:
         c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
         c.action_space.kinematics = "unicycle"
-    return make_cn_config(c, num_envs=E, env_offset=env_offset, nenv=nenv, phase="train")
+    return make_cn_config(c, num_envs=E, env_offset=env_offset, nenv=nenv, phase="train", rng=rng)
 
 
-def engines_for(workload, E, N, rank, world):
+def engines_for(workload, E, N, rank, world, rng="mt19937"):
     """(list of cn_config, per-engine action kind) for one rank. C5: per-env scenario
     dispatch round-robin over {parallel, perpendicular} traffic (N = 5) and the three side-preference
     scenarios (N = 1, circle radius 4, fixed robot), norm-zone reward and social metrics on: one engine
@@ -73,7 +73,7 @@ def engines_for(workload, E, N, rank, world):
     from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config
 
     if workload != "c5":
-        return [(make_config(E, N, rank * E, E * world, workload), workload)]
+        return [(make_config(E, N, rank * E, E * world, workload, rng), workload)]
     out = []
     half = E // 2
     for k, (scen, n) in enumerate(((["parallel_traffic", "perpendicular_traffic"], 5),
@@ -89,7 +89,8 @@ def engines_for(workload, E, N, rank, world):
             c.sim.circle_radius = 4
             c.humans.random_goal_changing = False
             c.humans.end_goal_changing = False
-        out.append((make_cn_config(c, num_envs=half, env_offset=rank * half, nenv=half * world, phase="train"), "c5"))
+        out.append((make_cn_config(c, num_envs=half, env_offset=rank * half, nenv=half * world, phase="train",
+                                   rng=rng), "c5"))
     return out
 
 
@@ -214,6 +215,9 @@ def main():
     ap.add_argument("--humans", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--rng", choices=["mt19937", "philox"], default="mt19937",
+                    help="reset / goal-change stream: mt19937 = the reference's numpy draws (default, the "
+                         "BASELINE line), philox = fast mode (SURVEY §8f-2)")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 = BASELINE metric (default); c3 / c4 / c5 are the SURVEY §8d side measurements "
                          "(c4: --steps / --warmup count PPO updates)")
@@ -243,7 +247,7 @@ def main():
         N = 25
     if args.workload == "c5" and E == 4096:
         E = 8192
-    engs = [CrowdNavEngine(cfg, device) for cfg, _ in engines_for(args.workload, E, N, rank, world)]
+    engs = [CrowdNavEngine(cfg, device) for cfg, _ in engines_for(args.workload, E, N, rank, world, args.rng)]
     eng = engs[0]
     gen = torch.Generator(device=device)
     gen.manual_seed(rank)
@@ -309,6 +313,7 @@ def main():
                 "envs_per_gpu": E_total, "humans": N if args.workload != "c5" else "5 / 1",
                 "global_envs": E_total * world,
                 "parallelism": "env-sharded x%d (no collective)" % world,
+                "rng": args.rng,
                 "step_kernel_ms": round(kernel_s * 1e3, 5),
             },
             "roofline": {

@@ -14,6 +14,8 @@ POLICY_ORCA, POLICY_SOCIAL_FORCE = 0, 1
 PHASE_TRAIN, PHASE_VAL, PHASE_TEST = 0, 1, 2
 PHASES = {"train": PHASE_TRAIN, "val": PHASE_VAL, "test": PHASE_TEST}
 SCMODE_ROUND_ROBIN, SCMODE_SEQUENTIAL = 0, 1
+RNG_MT19937, RNG_PHILOX = 0, 1   # include/crowdnav.h CN_RNG_*
+RNG_MODE = {"mt19937": RNG_MT19937, "philox": RNG_PHILOX}
 
 SCENARIOS = [
     "circle_crossing",
@@ -103,7 +105,7 @@ class CnConfig(ctypes.Structure):
         ("sf_B", ctypes.c_double),
         ("sf_KI", ctypes.c_double),
         ("max_tries", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("rng_mode", ctypes.c_int32),
     ]
 
     def copy(self):

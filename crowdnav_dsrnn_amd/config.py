@@ -163,10 +163,13 @@ class UnsupportedConfig(ValueError):
 
 
 def make_cn_config(config, num_envs, env_offset=0, nenv=None, phase=None, seed=None, max_tries=1000,
-                   scenarios=None, scenario_mode=None):
+                   scenarios=None, scenario_mode=None, rng=None):
     """Translate a reference-style config into `cn_config` for `num_envs` envs starting at global
     index `env_offset`; `nenv` is the reference's num_processes over all shards (make_env's envNum,
-    pytorchBaselines/a2c_ppo_acktr/envs.py:66-73); `phase` defaults like make_env ('train' if nenv > 1)."""
+    pytorchBaselines/a2c_ppo_acktr/envs.py:66-73); `phase` defaults like make_env ('train' if nenv > 1).
+    `rng` ('mt19937' default = the reference's numpy draws, or 'philox' = fast mode with the same draw
+    order and distributions; also read from `config.env.rng` when set) selects the reset / goal-change
+    random stream."""
     nenv = num_envs if nenv is None else nenv
     if phase is None:
         phase = "train" if nenv > 1 else "test"
@@ -256,6 +259,10 @@ def make_cn_config(config, num_envs, env_offset=0, nenv=None, phase=None, seed=N
     c.sf_B = float(config.sf.B)
     c.sf_KI = float(config.sf.KI)
     c.max_tries = int(max_tries)
+    rng = getattr(config.env, "rng", "mt19937") if rng is None else rng
+    if rng not in abi.RNG_MODE:
+        raise UnsupportedConfig("rng=%r (one of %s)" % (rng, sorted(abi.RNG_MODE)))
+    c.rng_mode = abi.RNG_MODE[rng]
     return c
 
 

@@ -782,16 +782,22 @@ __device__ __forceinline__ double mt_dbl(const uint32_t *w, int q)
     return (a * 67108864.0 + b) / 9007199254740992.0;
 }
 
+// CN_RNG_PHILOX (`phx`): word q is philox(q >> 2) under the episode key (`key`, also kept in w[0] for the
+// state write-back); the ring is unused, p counts words from the reset and ensure() is a no-op.
 struct WRng {
     double *sl;    // LDS [6][64] per-try candidate slots (wave_reject2)
     uint32_t *w;   // LDS [2*624]
-    int p;         // stream position (wave-uniform), 0 .. 2*624
+    int p;         // stream position (wave-uniform), 0 .. 2*624 (MT19937) / words since the reset (Philox)
     bool have1;    // block 1 generated
     bool slid;     // the key advanced by at least one whole block (key words must be written back)
+    bool phx;      // CN_RNG_PHILOX
+    uint32_t key;  // Philox key word 0 (the episode seed)
     int lane;
+    __device__ double dbl(int q) const { return phx ? philox_dbl(key, q) : mt_dbl(w, q); }
     // make words [p, p + need) readable (need <= 624); all lanes call it together
     __device__ void ensure(int need)
     {
+        if (phx) return;
         if (p + need > CN_MT_N && !have1) { mt_gen_wave(w, w + CN_MT_N, lane); have1 = true; }
         if (p + need > 2 * CN_MT_N) {
             for (int k = lane; k < CN_MT_N; k += 64) w[k] = w[CN_MT_N + k];
@@ -801,7 +807,7 @@ struct WRng {
             slid = true;
         }
     }
-    __device__ double rnd() { ensure(2); const double d = mt_dbl(w, p); p += 2; return d; }
+    __device__ double rnd() { ensure(2); const double d = dbl(p); p += 2; return d; }
     __device__ double unif(double lo, double hi) { return lo + (hi - lo) * rnd(); }
 };
 
@@ -817,20 +823,20 @@ __host__ __device__ inline int cand_words(int scenario)
 }
 
 // create_agent_attributes from the words starting at q
-__device__ void cand_attributes(const cn_config &c, const uint32_t *w, int q, int scenario, double agent_vpref,
+__device__ void cand_attributes(const cn_config &c, const WRng &w, int q, int scenario, double agent_vpref,
                                 double agent_radius, double robot_radius, double &px, double &py, double &gx,
                                 double &gy, double &heading, double &vp)
 {
     double v_pref = agent_vpref == 0 ? 1.0 : agent_vpref;
-    const double pxn = (mt_dbl(w, q) - 0.5) * v_pref;
-    const double pyn = (mt_dbl(w, q + 2) - 0.5) * v_pref;
+    const double pxn = (w.dbl(q) - 0.5) * v_pref;
+    const double pyn = (w.dbl(q + 2) - 0.5) * v_pref;
     q += 4;
     const double R = c.circle_radius;
-    auto rwp = [&](int qq) { return (mt_dbl(w, qq) - 0.5) * c.square_width / 2; };
+    auto rwp = [&](int qq) { return (w.dbl(qq) - 0.5) * c.square_width / 2; };
     heading = 0;
     switch (scenario) {
     case CN_SC_CIRCLE_CROSSING: {
-        const double angle = mt_dbl(w, q) * CN_PI * 2;
+        const double angle = w.dbl(q) * CN_PI * 2;
         px = R * cos(angle) + pxn; py = R * sin(angle) + pyn;
         gx = -px; gy = -py;
     } break;
@@ -841,14 +847,14 @@ __device__ void cand_attributes(const cn_config &c, const uint32_t *w, int q, in
         gy = rwp(q + 6) * 0.4 + pyn;
         break;
     case CN_SC_PARALLEL_TRAFFIC: {
-        const double sign = mt_dbl(w, q) >= 0.5 ? 1 : -1;
+        const double sign = w.dbl(q) >= 0.5 ? 1 : -1;
         px = rwp(q + 2) * 0.4 + pxn;
-        py = sign * (mt_dbl(w, q + 4) * 3 + 1 + pyn);
+        py = sign * (w.dbl(q + 4) * 3 + 1 + pyn);
         gx = px; gy = -py;
     } break;
     case CN_SC_PERPENDICULAR_TRAFFIC: {
-        const double sign = mt_dbl(w, q) >= 0.5 ? 1 : -1;
-        px = sign * (mt_dbl(w, q + 2) * 3 + 1 + pxn);
+        const double sign = w.dbl(q) >= 0.5 ? 1 : -1;
+        px = sign * (w.dbl(q + 2) * 3 + 1 + pxn);
         gx = -px;
         py = rwp(q + 4) * 0.4 + pyn;
         gy = py;
@@ -856,14 +862,14 @@ __device__ void cand_attributes(const cn_config &c, const uint32_t *w, int q, in
     case CN_SC_SIDE_PREF_PASSING:
     case CN_SC_SIDE_PREF_OVERTAKING: {
         const double min_x = -(robot_radius + agent_radius), max_x = -min_x;
-        const double hx = (max_x - min_x) * mt_dbl(w, q) + min_x;
+        const double hx = (max_x - min_x) * w.dbl(q) + min_x;
         px = hx; gx = hx;
         if (scenario == CN_SC_SIDE_PREF_PASSING) { py = R; gy = -R; heading = -CN_PI / 2; }
         else { py = -R + 2; gy = R + 2; heading = CN_PI / 2; v_pref = 0.3; }
     } break;
     default: {
         const double min_x = -(R + robot_radius + agent_radius), max_x = -(R - robot_radius - agent_radius);
-        const double hx = (max_x - min_x) * mt_dbl(w, q) + min_x;
+        const double hx = (max_x - min_x) * w.dbl(q) + min_x;
         px = hx; gx = -hx; py = 0; gy = 0;
     } break;
     }
@@ -956,15 +962,22 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
     uint32_t *mtw = m.w;
     if (c.scenario_mode == CN_SCMODE_SEQUENTIAL) sc = c.scenarios[reset_count % c.num_scenarios];
     else sc = c.scenarios[gidx % c.num_scenarios];
-    if (lane == 0) {
-        uint32_t seed = (uint32_t)(counter_offset + case_counter + (c.seed + gidx));
-        for (int k = 0; k < CN_MT_N; ++k) {  // mt19937_seed: sequential Knuth chain
-            mtw[k] = seed;
-            seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(k + 1);
+    const uint32_t seed0 = (uint32_t)(counter_offset + case_counter + (c.seed + gidx));
+    if (m.phx) {
+        if (lane == 0) mtw[0] = seed0;   // the key is the whole stream state (written back with the reset)
+        m.key = seed0;
+        m.p = 0;
+    } else {
+        if (lane == 0) {
+            uint32_t seed = seed0;
+            for (int k = 0; k < CN_MT_N; ++k) {  // mt19937_seed: sequential Knuth chain
+                mtw[k] = seed;
+                seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(k + 1);
+            }
         }
+        m.p = CN_MT_N;   // numpy: pos = 624 after seeding, the first draw runs mt19937_gen
     }
     wsync();
-    m.p = CN_MT_N;   // numpy: pos = 624 after seeding, the first draw runs mt19937_gen
     m.have1 = false; m.slid = false;
     ovf = 0;
     const double R = c.circle_radius;
@@ -974,7 +987,7 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
         en.rpx = R * cos(angle); en.rpy = R * sin(angle);
         // goal: uniform in the square until >= 6 m away (crowd_sim.py:620-634)
         const int tw = wave_reject2(m, 4, 1, c.max_tries, ovf, [&](int q, int t) {
-            m.sl[t] = -R + (R - -R) * mt_dbl(mtw, q); m.sl[64 + t] = -R + (R - -R) * mt_dbl(mtw, q + 2);
+            m.sl[t] = -R + (R - -R) * m.dbl(q); m.sl[64 + t] = -R + (R - -R) * m.dbl(q + 2);
         }, [&](int t, int) { return norm_lt(en.rpx - m.sl[t], en.rpy - m.sl[64 + t], 6.0); });
         en.rgx = m.sl[tw]; en.rgy = m.sl[64 + tw];
         wsync();
@@ -984,8 +997,8 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
     } else {
         // holonomic robot: start and goal uniform in the square until >= 6 m apart (crowd_sim.py:652-660)
         const int tw = wave_reject2(m, 8, 1, c.max_tries, ovf, [&](int q, int t) {
-            m.sl[t] = -R + (R - -R) * mt_dbl(mtw, q); m.sl[64 + t] = -R + (R - -R) * mt_dbl(mtw, q + 2);
-            m.sl[128 + t] = -R + (R - -R) * mt_dbl(mtw, q + 4); m.sl[192 + t] = -R + (R - -R) * mt_dbl(mtw, q + 6);
+            m.sl[t] = -R + (R - -R) * m.dbl(q); m.sl[64 + t] = -R + (R - -R) * m.dbl(q + 2);
+            m.sl[128 + t] = -R + (R - -R) * m.dbl(q + 4); m.sl[192 + t] = -R + (R - -R) * m.dbl(q + 6);
         }, [&](int t, int) { return norm_lt(m.sl[t] - m.sl[128 + t], m.sl[64 + t] - m.sl[192 + t], 6.0); });
         en.rpx = m.sl[tw]; en.rpy = m.sl[64 + tw]; en.rgx = m.sl[128 + tw]; en.rgy = m.sl[192 + tw];
         wsync();
@@ -998,7 +1011,7 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
         // candidate vs the robot and the humans placed so far (crowd_sim.py:369-390): i + 1 agent tests
         const int tw = wave_reject2(m, W, i + 1, c.max_tries, ovf, [&](int q, int t) {
             double px, py, gx, gy, hd, vp;
-            cand_attributes(c, mtw, q, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
+            cand_attributes(c, m, q, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
             m.sl[t] = px; m.sl[64 + t] = py; m.sl[128 + t] = gx; m.sl[192 + t] = gy; m.sl[256 + t] = hd;
             m.sl[320 + t] = vp;
         }, [&](int t, int a) {
@@ -1025,12 +1038,13 @@ __device__ __forceinline__ void write_pending(const PendPtrs &P, const cn_config
                               int sc, uint32_t ovf, const uint32_t *mt_src, int pos, int64_t cc, int32_t rc, int lane)
 {
     const int N = c.human_num;
+    const int nk = c.rng_mode == CN_RNG_PHILOX ? 1 : CN_MT_N;   // key words to copy
     {
         uint32_t v[(CN_MT_N + 63) / 64];
 #pragma unroll
-        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; v[j] = k < CN_MT_N ? mt_src[k] : 0u; }
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; v[j] = k < nk ? mt_src[k] : 0u; }
 #pragma unroll
-        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; if (k < CN_MT_N) P.mt[e * CN_MT_N + k] = v[j]; }
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; if (k < nk) P.mt[e * CN_MT_N + k] = v[j]; }
     }
     if (lane < N) {
         const int64_t h = e * N + lane, EN = E * N;
@@ -1078,12 +1092,13 @@ __device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &
     }
     const int A = N + (c.robot_visible ? 1 : 0);
     if (A > 10) for (int k = lane; k < N * A; k += 64) S.o_perm[e * N * A + k] = 0;
+    const int nk = c.rng_mode == CN_RNG_PHILOX ? 1 : CN_MT_N;   // key words to copy
     {   // all loads first, then all stores: mt_src may be LDS or global, so the compiler cannot pipeline
         uint32_t v[(CN_MT_N + 63) / 64];
 #pragma unroll
-        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; v[j] = k < CN_MT_N ? mt_src[k] : 0u; }
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; v[j] = k < nk ? mt_src[k] : 0u; }
 #pragma unroll
-        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; if (k < CN_MT_N) S.mt[e * CN_MT_N + k] = v[j]; }
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; if (k < nk) S.mt[e * CN_MT_N + k] = v[j]; }
     }
     if (lane == 0) {
         S.scenario[e] = (int32_t)sc;
@@ -1120,7 +1135,6 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
 {
     int dbg = 0;   // diagnostics: 1000 * rounds + eligible humans + 100 * changes
     const int N = c.human_num, lane = m.lane;
-    uint32_t *mtw = m.w;
     double *ngx = sp, *ngy = sp + 32, *nr = sp + 64;
     const double chance = KIND == 0 ? c.goal_change_chance : c.end_goal_change_chance;
     const int W = KIND == 0 ? 6 : cand_words(sc);
@@ -1147,7 +1161,7 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
         if (n * (n + 1) / 2 <= 64) {
             int k = 0, cc = lane;
             while (cc > k) { cc -= k + 1; ++k; }
-            const bool dec = lane < n * (n + 1) / 2 && mt_dbl(mtw, p0 + 2 * k + SW * cc) <= chance;
+            const bool dec = lane < n * (n + 1) / 2 && m.dbl(p0 + 2 * k + SW * cc) <= chance;
             const uint64_t B = __ballot(dec);
             uint64_t mm = rem;
             for (int kk = 0; kk < n; ++kk) {
@@ -1163,7 +1177,7 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
             int p = p0;
             for (int i = i0; i < N; ++i) {
                 if (!((rem >> i) & 1ull)) continue;
-                const double U = mt_dbl(mtw, p);
+                const double U = m.dbl(p);
                 p += 2;
                 if (U <= chance) {
                     chg |= 1ull << i;
@@ -1185,15 +1199,15 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
             r_i = en.hr[lane]; vp_i = en.hvp[lane];
             if (KIND == 0) {
                 const double vp = en.hvp[lane] == 0 ? 1.0 : en.hvp[lane];
-                const double angle = mt_dbl(mtw, q) * CN_PI * 2;
-                const double gxn = (mt_dbl(mtw, q + 2) - 0.5) * vp, gyn = (mt_dbl(mtw, q + 4) - 0.5) * vp;
+                const double angle = m.dbl(q) * CN_PI * 2;
+                const double gxn = (m.dbl(q + 2) - 0.5) * vp, gyn = (m.dbl(q + 4) - 0.5) * vp;
                 gx = c.circle_radius * cos(angle) + gxn;
                 gy = c.circle_radius * sin(angle) + gyn;
             } else {
-                if (c.random_radii) { r_i += -0.1 + (0.1 - -0.1) * mt_dbl(mtw, q); q += 2; }
-                if (c.random_v_pref) { vp_i += -0.1 + (0.1 - -0.1) * mt_dbl(mtw, q); q += 2; }
+                if (c.random_radii) { r_i += -0.1 + (0.1 - -0.1) * m.dbl(q); q += 2; }
+                if (c.random_v_pref) { vp_i += -0.1 + (0.1 - -0.1) * m.dbl(q); q += 2; }
                 double px, py, hd, vpo;
-                cand_attributes(c, mtw, q, sc, vp_i, r_i, en.rr, px, py, gx, gy, hd, vpo);
+                cand_attributes(c, m, q, sc, vp_i, r_i, en.rr, px, py, gx, gy, hd, vpo);
             }
             ngx[lane] = gx; ngy[lane] = gy; nr[lane] = r_i;
         }
@@ -1252,13 +1266,13 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
         const int tw = wave_reject2(m, W, NA, c.max_tries, ovf, [&](int q, int t) {
             double gx, gy;
             if (KIND == 0) {
-                const double angle = mt_dbl(mtw, q) * CN_PI * 2;
-                const double gxn = (mt_dbl(mtw, q + 2) - 0.5) * vpk0, gyn = (mt_dbl(mtw, q + 4) - 0.5) * vpk0;
+                const double angle = m.dbl(q) * CN_PI * 2;
+                const double gxn = (m.dbl(q + 2) - 0.5) * vpk0, gyn = (m.dbl(q + 4) - 0.5) * vpk0;
                 gx = c.circle_radius * cos(angle) + gxn;
                 gy = c.circle_radius * sin(angle) + gyn;
             } else {
                 double px, py, hd, vp;
-                cand_attributes(c, mtw, q, sc, vpf, rf, en.rr, px, py, gx, gy, hd, vp);
+                cand_attributes(c, m, q, sc, vpf, rf, en.rr, px, py, gx, gy, hd, vp);
             }
             m.sl[t] = gx; m.sl[64 + t] = gy;
         }, [&](int t, int a) { return goal_hit(c, en, f, r_self, m.sl[t], m.sl[64 + t], a); });
@@ -1280,7 +1294,8 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
     const int lane = m.lane;
     uint32_t *mtw = m.w;
     const int64_t hb = e * N;
-    {
+    if (m.phx) m.key = S.mt[e * CN_MT_N];
+    else {
         uint32_t v[(CN_MT_N + 63) / 64];
 #pragma unroll
         for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; v[j] = k < CN_MT_N ? S.mt[e * CN_MT_N + k] : 0u; }
@@ -1303,7 +1318,7 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
 #endif
     (void)dbg0; (void)dbg1;
     // numpy twists lazily: a stream that consumed exactly the 624 words is (old key, pos 624)
-    const bool in1 = m.p > CN_MT_N;
+    const bool in1 = !m.phx && m.p > CN_MT_N;
     if (lane < N) {
         S.h_gx[hb + lane] = en.hgx[lane]; S.h_gy[hb + lane] = en.hgy[lane];
         S.h_r[hb + lane] = en.hr[lane]; S.h_vpref[hb + lane] = en.hvp[lane];
@@ -1344,7 +1359,7 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P, 
         uint32_t ovf;
         int sc;
         spawn_env(c, c.env_offset + e, cc, rc, counter_offset, m, en, rth, ovf, sc);
-        const bool in1 = m.p > CN_MT_N;
+        const bool in1 = !m.phx && m.p > CN_MT_N;
         write_reset(o, c, e, en, rth, sc, ovf, m.w + (in1 ? CN_MT_N : 0), in1 ? m.p - CN_MT_N : m.p, lane);
     }
     wsync();
@@ -1362,6 +1377,7 @@ struct PendLaunch {
     int64_t counter_offset;
 };
 
+template <bool PHX>
 __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_ptrs &S, const cn_config &c, int E, char *smem)
 {
     const int nw = pl.waves, w = threadIdx.x / 64, lane = threadIdx.x & 63;
@@ -1376,7 +1392,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
         en.hth = hb + 192;
         WRng m;
-        m.w = mtw; m.lane = lane;
+        m.w = mtw; m.lane = lane; m.phx = PHX;
         m.sl = (double *)(base + 2 * CN_MT_N * 4 + 7 * 32 * 8);
         const int64_t cc = S.case_counter[e];
         const int32_t rc = S.reset_count[e];
@@ -1384,7 +1400,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         uint32_t ovf;
         int sc;
         spawn_env(c, c.env_offset + e, cc, rc, pl.counter_offset, m, en, rth, ovf, sc);
-        const bool in1 = m.p > CN_MT_N;
+        const bool in1 = !m.phx && m.p > CN_MT_N;
         write_pending(pl.P, c, E, e, en, rth, sc, ovf, mtw + (in1 ? CN_MT_N : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
                       lane);
         wsync();
@@ -1443,12 +1459,14 @@ __device__ inline float bbox_dist(float x, float y, float mnx, float mxx, float 
     return a * a + b * b + cc * cc + d * d;
 }
 
-template <bool KD>
+// KD: RVO2 kd-tree neighbour order (> 10 agents per simulator); PHX: c.rng_mode == CN_RNG_PHILOX, a
+// template argument so that the MT19937 build carries no Philox registers
+template <bool KD, bool PHX>
 __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g, cn_config c)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if ((int)blockIdx.x >= g.pend.step_blocks) {  // spare workgroups: draw upcoming episodes' spawns
-        pend_waves(g.pend, g.s, c, g.E, smem);
+        pend_waves<PHX>(g.pend, g.s, c, g.E, smem);
         return;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *g.pcount_zero = 0u;
@@ -2200,7 +2218,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const int nw = P.rng_waves, w = tid / 64, lane = tid & 63;
         char *wb = smem + P.o_lines + (w < nw ? w : 0) * CN_PEND_LDS;   // over the ORCA scratch, dead after phase 2
         WRng m;
-        m.w = (uint32_t *)wb; m.lane = lane;
+        m.w = (uint32_t *)wb; m.lane = lane; m.phx = PHX;
         m.sl = (double *)(wb + 2 * CN_MT_N * 4 + 7 * 32 * 8);
         double *hb = (double *)(wb + 2 * CN_MT_N * 4);
         ResetOut o;
@@ -2250,7 +2268,7 @@ __global__ void __launch_bounds__(64) cn_reset_kernel(RngArgs g, cn_config c)
         en.hpx = hbuf[0]; en.hpy = hbuf[1]; en.hgx = hbuf[2]; en.hgy = hbuf[3]; en.hr = hbuf[4]; en.hvp = hbuf[5];
         en.hth = hbuf[6];
         WRng m;
-        m.w = mtw; m.lane = lane; m.sl = slots;
+        m.w = mtw; m.lane = lane; m.sl = slots; m.phx = c.rng_mode == CN_RNG_PHILOX;
         reset_env(g.o, g.pend, c, g.E, e, g.counter_offset, true, m, en);
     }
 }
@@ -2514,6 +2532,7 @@ int cn_config_validate(const cn_config *c)
     for (int k = 0; k < c->num_scenarios; ++k)
         if (c->scenarios[k] < 0 || c->scenarios[k] > CN_SC_SIDE_PREF_CROSSING) return set_err(CN_EINVAL, "scenario id");
     if (c->kinematics != CN_HOLONOMIC && c->kinematics != CN_UNICYCLE) return set_err(CN_EINVAL, "kinematics");
+    if (c->rng_mode != CN_RNG_MT19937 && c->rng_mode != CN_RNG_PHILOX) return set_err(CN_EINVAL, "rng_mode");
     if (c->human_policy != CN_POLICY_ORCA && c->human_policy != CN_POLICY_SOCIAL_FORCE)
         return set_err(CN_EUNSUPPORTED, "human policy");
     if (!c->potential_based) return set_err(CN_EUNSUPPORTED, "only potential-based reward shaping is supported");
@@ -2632,10 +2651,9 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     }
     if (g->a_lds > 160 * 1024) { cn_destroy(g); return set_err(CN_EUNSUPPORTED, "LDS plan exceeds 160 KiB"); }
     if (g->a_lds > 64 * 1024) {
-        (void)hipFuncSetAttribute((const void *)cn_step_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  g->a_lds);
-        (void)hipFuncSetAttribute((const void *)cn_step_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  g->a_lds);
+        const void *ks[4] = {(const void *)cn_step_kernel<true, false>, (const void *)cn_step_kernel<false, false>,
+                             (const void *)cn_step_kernel<true, true>, (const void *)cn_step_kernel<false, true>};
+        for (const void *k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g->a_lds);
     }
     g->rng_grid = g->E < 2048 ? g->E : 2048;
     HIPCHK(hipDeviceSynchronize());
@@ -2736,10 +2754,15 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.pend.waves = g->pend_waves;
     g->pend_all = 0;
     const int grid = blocks + g->pend_blocks;
-    if (g->plan.kd)
-        hipLaunchKernelGGL(cn_step_kernel<true>, dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
+    const bool phx = g->c.rng_mode == CN_RNG_PHILOX;
+    if (g->plan.kd && phx)
+        hipLaunchKernelGGL((cn_step_kernel<true, true>), dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
+    else if (g->plan.kd)
+        hipLaunchKernelGGL((cn_step_kernel<true, false>), dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
+    else if (phx)
+        hipLaunchKernelGGL((cn_step_kernel<false, true>), dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
     else
-        hipLaunchKernelGGL(cn_step_kernel<false>, dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
+        hipLaunchKernelGGL((cn_step_kernel<false, false>), dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
     HIPCHK(hipGetLastError());
     if (prof && ++g->prof_n == g->prof_cap) HIPCHK(hipEventRecord(g->ev[1], st));
     return CN_OK;

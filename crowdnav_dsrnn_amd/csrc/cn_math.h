@@ -102,4 +102,30 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b, uint32_t c)
     return c ^ (y >> 1) ^ ((0u - (y & 1u)) & 0x9908b0dfu);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11; the Random123 constants) for CN_RNG_PHILOX. Word q of an episode's
+// stream is word (q & 3) of philox(counter = (q >> 2, 0, 0, 0), key = (seed, CN_PHILOX_K1)); a double is
+// two consecutive words converted like numpy's random_sample ((a >> 5) * 2^26 + (b >> 6)) / 2^53.
+// Draws always start at even word positions, so both words of a double come from one counter block.
+// ---------------------------------------------------------------------------------------------
+#define CN_PHILOX_K1 0x43726f77u
+__device__ __forceinline__ uint4 philox4x32_10(uint32_t c0, uint32_t k0, uint32_t k1)
+{
+    uint32_t x0 = c0, x1 = 0, x2 = 0, x3 = 0;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = 0xD2511F53u * x0, hi0 = __umulhi(0xD2511F53u, x0);
+        const uint32_t lo1 = 0xCD9E8D57u * x2, hi1 = __umulhi(0xCD9E8D57u, x2);
+        x0 = hi1 ^ x1 ^ k0; x1 = lo1; x2 = hi0 ^ x3 ^ k1; x3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return make_uint4(x0, x1, x2, x3);
+}
+__device__ __forceinline__ double philox_dbl(uint32_t key, int q)
+{
+    const uint4 w = philox4x32_10((uint32_t)q >> 2, key, CN_PHILOX_K1);
+    const uint32_t a = (q & 2) ? w.z : w.x, b = (q & 2) ? w.w : w.y;
+    return ((int32_t)(a >> 5) * 67108864.0 + (int32_t)(b >> 6)) / 9007199254740992.0;
+}
+
 }  // namespace cn

@@ -73,6 +73,10 @@ extern "C" {
 /* scenario selection at reset (crowd_sim_dict.py:110-125) */
 #define CN_SCMODE_ROUND_ROBIN 0  /* env g uses scenarios[g % n]; n == 1 is the deterministic reference case */
 #define CN_SCMODE_SEQUENTIAL 1   /* test.social_metrics: scenarios[reset_count % n] (crowd_sim_dict.py:114-122) */
+/* random stream of resets and goal changes (crowd_sim_dict.py:154 reseeds numpy's global RandomState) */
+#define CN_RNG_MT19937 0  /* parity: numpy legacy MT19937 per env, the reference's exact draws */
+#define CN_RNG_PHILOX 1   /* fast mode: Philox4x32-10, key (episode seed, 0x43726f77), counter = word / 4;
+                             same draw order and distributions, different values; no 2.5 KB key per env */
 /* step events (crowd_sim/envs/utils/info.py) */
 #define CN_EV_NOTHING 0
 #define CN_EV_DANGER 1
@@ -131,7 +135,7 @@ typedef struct cn_config {
     double sf_A, sf_B, sf_KI;
     /* engine */
     int32_t max_tries;     /* bounded rejection sampling (reference loops forever) */
-    int32_t reserved;
+    int32_t rng_mode;      /* CN_RNG_MT19937 (default) / CN_RNG_PHILOX */
 } cn_config;
 
 typedef struct cn_engine cn_engine;

@@ -30,7 +30,8 @@
  *   ep_*       baselines bench.Monitor episode accumulators (consumed at train.py:266-267)
  *   case_counter  CrowdSim.case_counter[phase]   crowd_sim_dict.py:136-164
  *   mt, mt_pos numpy RandomState (legacy MT19937) global stream, reseeded at every reset
- *              crowd_sim_dict.py:154
+ *              crowd_sim_dict.py:154. CN_RNG_PHILOX: mt[0] = the episode's Philox key word, mt_pos =
+ *              words consumed since the reset (the other 623 words are unused)
  */
 #ifndef CROWDNAV_STATE_H
 #define CROWDNAV_STATE_H

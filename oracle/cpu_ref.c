@@ -152,16 +152,59 @@ static double mt_double(uint32_t *mt, int32_t *pos)
     return (a * 67108864.0 + b) / 9007199254740992.0;
 }
 
-typedef struct { uint32_t *mt; int32_t *pos; } rng_t;
-static inline double rnd(rng_t r) { return mt_double(r.mt, r.pos); }                       /* np.random.random() */
+/* CN_RNG_PHILOX fast mode (include/crowdnav.h): Philox4x32-10 as published by Salmon, Moraes, Dror &
+ * Shaw (SC'11) / Random123 (multipliers 0xD2511F53, 0xCD9E8D57; Weyl key bumps 0x9E3779B9, 0xBB67AE85),
+ * key (episode seed, 0x43726f77), counter (word >> 2, 0, 0, 0); a double is two consecutive words with
+ * numpy's random_sample conversion. Restated here independently of the HIP engine's copy. */
+static void philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4])
+{
+    uint32_t x[4] = {ctr[0], ctr[1], ctr[2], ctr[3]}, k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * x[0], p1 = (uint64_t)0xCD9E8D57u * x[2];
+        const uint32_t y0 = (uint32_t)(p1 >> 32) ^ x[1] ^ k0, y1 = (uint32_t)p1;
+        const uint32_t y2 = (uint32_t)(p0 >> 32) ^ x[3] ^ k1, y3 = (uint32_t)p0;
+        x[0] = y0; x[1] = y1; x[2] = y2; x[3] = y3;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    memcpy(out, x, sizeof x);
+}
+EXPORT void cnref_philox4x32_10(const uint32_t *ctr, const uint32_t *key, uint32_t *out)
+{ /* test hook: Random123 known-answer vectors */
+    philox4x32_10(ctr, key, out);
+}
+static double philox_double(uint32_t key, int32_t *pos)
+{
+    uint32_t w[4];
+    const uint32_t ctr[4] = {(uint32_t)*pos >> 2, 0, 0, 0}, k[2] = {key, 0x43726f77u};
+    philox4x32_10(ctr, k, w);
+    const int o = *pos & 3;   /* 0 or 2: draws start at even words */
+    *pos += 2;
+    const int32_t a = (int32_t)(w[o] >> 5), b = (int32_t)(w[o + 1] >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
+
+/* an env's stream: MT19937 key words + position, or (philox) the key in mt[0] + words drawn since reset */
+typedef struct { uint32_t *mt; int32_t *pos; int philox; } rng_t;
+static inline double rnd(rng_t r)                                                            /* np.random.random() */
+{
+    return r.philox ? philox_double(r.mt[0], r.pos) : mt_double(r.mt, r.pos);
+}
 static inline double unif(rng_t r, double lo, double hi) { return lo + (hi - lo) * rnd(r); } /* np.random.uniform */
+
+EXPORT void cnref_philox_draw(uint32_t key, int n, double *out)
+{ /* test hook: the first n doubles of the Philox stream of episode seed `key` */
+    uint32_t mt[1] = {key};
+    int32_t pos = 0;
+    rng_t r = {mt, &pos, 1};
+    for (int i = 0; i < n; ++i) out[i] = rnd(r);
+}
 
 EXPORT void cnref_mt_draw(uint32_t seed, int n, double *out)
 { /* test hook: np.random.seed(seed); [np.random.random() for _ in range(n)] */
     uint32_t mt[CN_MT_N];
     int32_t pos;
     mt_seed(mt, &pos, seed);
-    rng_t r = {mt, &pos};
+    rng_t r = {mt, &pos, 0};
     for (int i = 0; i < n; ++i) out[i] = rnd(r);
 }
 
@@ -776,7 +819,7 @@ static void env_reset(ref_engine *g, int e, float *robot_node, float *temporal, 
 {
     const int N = g->N;
     const int64_t gidx = g->c.env_offset + e;
-    rng_t r = {&g->s.mt[(int64_t)e * CN_MT_N], &g->s.mt_pos[e]};
+    rng_t r = {&g->s.mt[(int64_t)e * CN_MT_N], &g->s.mt_pos[e], g->c.rng_mode == CN_RNG_PHILOX};
     /* scenario choice (crowd_sim_dict.py:110-125); the unseeded random.choices is replaced by a
      * deterministic assignment (identical to the reference when one scenario is configured) */
     int sc;
@@ -786,7 +829,8 @@ static void env_reset(ref_engine *g, int e, float *robot_node, float *temporal, 
     R1(gtime, e) = 0.0;
     R1(r_dv, e) = 0.0;
     const int64_t seed = g->counter_offset + R1(case_counter, e) + (g->c.seed + gidx);
-    mt_seed(r.mt, r.pos, (uint32_t)seed);
+    if (r.philox) { r.mt[0] = (uint32_t)seed; *r.pos = 0; }
+    else mt_seed(r.mt, r.pos, (uint32_t)seed);
     uint32_t ovf = 0;
     const double R = g->c.circle_radius;
     /* robot (crowd_sim.py:626-660) */
@@ -858,7 +902,7 @@ static void env_reset(ref_engine *g, int e, float *robot_node, float *temporal, 
 static void goals_randomly(ref_engine *g, int e)
 {
     const int N = g->N;
-    rng_t r = {&g->s.mt[(int64_t)e * CN_MT_N], &g->s.mt_pos[e]};
+    rng_t r = {&g->s.mt[(int64_t)e * CN_MT_N], &g->s.mt_pos[e], g->c.rng_mode == CN_RNG_PHILOX};
     for (int i = 0; i < N; ++i) {
         if (H(h_vpref, e, i) == 0) continue;
         if (rnd(r) <= g->c.goal_change_chance) {
@@ -890,7 +934,7 @@ static void goals_randomly(ref_engine *g, int e)
 static void human_goal(ref_engine *g, int e, int i)
 {
     const int N = g->N;
-    rng_t r = {&g->s.mt[(int64_t)e * CN_MT_N], &g->s.mt_pos[e]};
+    rng_t r = {&g->s.mt[(int64_t)e * CN_MT_N], &g->s.mt_pos[e], g->c.rng_mode == CN_RNG_PHILOX};
     if (rnd(r) <= g->c.end_goal_change_chance) {
         if (g->c.random_radii) H(h_r, e, i) += unif(r, -0.1, 0.1);
         if (g->c.random_v_pref) H(h_vpref, e, i) += unif(r, -0.1, 0.1);

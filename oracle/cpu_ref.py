@@ -36,6 +36,8 @@ def lib():
         L.cnref_get_state.argtypes = [vp, vp]
         L.cnref_set_state.argtypes = [vp, vp]
         L.cnref_mt_draw.argtypes = [ctypes.c_uint32, ctypes.c_int, vp]
+        L.cnref_philox_draw.argtypes = [ctypes.c_uint32, ctypes.c_int, vp]
+        L.cnref_philox4x32_10.argtypes = [vp, vp, vp]
         L.cnref_rvo2_agent0.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
                                         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp]
         L.cnref_set_threads.argtypes = [ctypes.c_int]
@@ -101,6 +103,20 @@ class RefEngine:
 def mt_draw(seed, n):
     out = np.zeros(n, np.float64)
     lib().cnref_mt_draw(seed, n, _p(out))
+    return out
+
+
+def philox_draw(key, n):
+    """First n doubles of the CN_RNG_PHILOX stream of episode seed `key`."""
+    out = np.zeros(n, np.float64)
+    lib().cnref_philox_draw(key, n, _p(out))
+    return out
+
+
+def philox4x32_10(ctr, key):
+    c, k = np.ascontiguousarray(ctr, np.uint32), np.ascontiguousarray(key, np.uint32)
+    out = np.zeros(4, np.uint32)
+    lib().cnref_philox4x32_10(_p(c), _p(k), _p(out))
     return out
 
 

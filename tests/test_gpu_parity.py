@@ -125,6 +125,15 @@ def _teacher_forced(gpu, oracle, cfg, kin, steps=60, seed=5):
     ("kd_tree_max_agents", "holonomic", 31, "orca", "square_crossing",
      {"robot__visible": True, "robot__FOV": 1.0, "humans__FOV": 1.0}),
     ("kd_tree_11_agents", "unicycle", 11, "orca", "circle_crossing", {"humans__FOV": 0.5}),
+    # CN_RNG_PHILOX fast mode: same draw order on both sides, so the same parity bar
+    ("philox_c2", "unicycle", 10, "orca", "circle_crossing", {"env__rng": "philox"}),
+    ("philox_kd_square_fov", "holonomic", 25, "orca", "square_crossing",
+     {"env__rng": "philox", "robot__FOV": 1.0, "humans__FOV": 1.0}),
+    ("philox_radii_vpref", "holonomic", 6, "orca", "circle_crossing",
+     {"env__rng": "philox", "humans__random_radii": True, "humans__random_v_pref": True}),
+    ("philox_social_metrics", "holonomic", 5, "orca",
+     ("parallel_traffic", "perpendicular_traffic", "circle_crossing", "square_crossing"),
+     {"env__rng": "philox", "test__social_metrics": True, "sim__circle_radius": 4}),
 ])
 def test_gpu_vs_oracle_configs(gpu, oracle, name, kin, N, policy, scen, over):
     """Teacher-forced GPU vs oracle over the option space the reference exposes (SURVEY §8d C5 shapes,
@@ -169,9 +178,11 @@ def test_gpu_vs_oracle_teacher_forced(gpu, oracle, kin, N, policy, scen, fov):
     assert mism <= cfg.num_envs * 60 * 0.001, mism
 
 
-def test_gpu_free_running_matches_oracle_short_horizon(gpu, oracle):
-    """Free-running (no teacher forcing) C2-shaped rollout: identical for the first 40 steps."""
-    cfg = _cfg(10, "unicycle", E=512)
+@pytest.mark.parametrize("rng", ["mt19937", "philox"])
+def test_gpu_free_running_matches_oracle_short_horizon(gpu, oracle, rng):
+    """Free-running (no teacher forcing) C2-shaped rollout: identical for the first 40 steps (auto-resets
+    from the spawns the spare workgroups draw ahead included)."""
+    cfg = _cfg(10, "unicycle", E=512, env__rng=rng)
     ref, g = oracle.RefEngine(cfg), gpu(cfg)
     o1, o2 = ref.reset(), g.reset()
     for k in o1:
