@@ -794,6 +794,9 @@ struct WRng {
     uint32_t key;  // Philox key word 0 (the episode seed)
     int lane;
     __device__ double dbl(int q) const { return phx ? philox_dbl(key, q) : mt_dbl(w, q); }
+    // R * cos(angle) with angle = rnd() * pi * 2 (crowd_sim.py:361, 736), for cand_attributes
+    __device__ double cos2pi(int q) const { return cos(dbl(q) * CN_PI * 2); }
+    __device__ double sin2pi(int q) const { return sin(dbl(q) * CN_PI * 2); }
     // make words [p, p + need) readable (need <= 624); all lanes call it together
     __device__ void ensure(int need)
     {
@@ -823,7 +826,8 @@ __host__ __device__ inline int cand_words(int scenario)
 }
 
 // create_agent_attributes from the words starting at q
-__device__ void cand_attributes(const cn_config &c, const WRng &w, int q, int scenario, double agent_vpref,
+template <typename Src>
+__device__ void cand_attributes(const cn_config &c, const Src &w, int q, int scenario, double agent_vpref,
                                 double agent_radius, double robot_radius, double &px, double &py, double &gx,
                                 double &gy, double &heading, double &vp)
 {
@@ -835,11 +839,10 @@ __device__ void cand_attributes(const cn_config &c, const WRng &w, int q, int sc
     auto rwp = [&](int qq) { return (w.dbl(qq) - 0.5) * c.square_width / 2; };
     heading = 0;
     switch (scenario) {
-    case CN_SC_CIRCLE_CROSSING: {
-        const double angle = w.dbl(q) * CN_PI * 2;
-        px = R * cos(angle) + pxn; py = R * sin(angle) + pyn;
+    case CN_SC_CIRCLE_CROSSING:
+        px = R * w.cos2pi(q) + pxn; py = R * w.sin2pi(q) + pyn;
         gx = -px; gy = -py;
-    } break;
+        break;
     case CN_SC_SQUARE_CROSSING:
         px = rwp(q) * 0.4 + pxn;
         py = rwp(q + 2) * 0.4 + pyn;
@@ -1118,168 +1121,141 @@ __device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &
 }
 
 
-// One of the two goal-change loops at the end of CrowdSimDict.step, evaluated speculatively:
+// Word page of a goal pass: the doubles of the next 128 stream words (64 draws) and, where the pass
+// needs angles, cos / sin of 2*pi*draw, computed by the 64 lanes at once (one draw + one f64 sincos per
+// lane) so that the sequential walk over the humans only reads tables. Index k holds the draw at word
+// pb + 2k. Wave-uniform reads are LDS broadcasts (v_readlane broadcasts of loop-carried values
+// miscompiled in this loop nest: wrong winners and NaN goals on the GPU, tools/diag_goal.py).
+struct GPage {
+    double *d, *cs, *sn;   // LDS [64] each (the wave's try-slot area m.sl, unused by the goal passes)
+    int pb;
+    __device__ double dbl(int q) const { return d[(q - pb) >> 1]; }
+    __device__ double cos2pi(int q) const { return cs[(q - pb) >> 1]; }
+    __device__ double sin2pi(int q) const { return sn[(q - pb) >> 1]; }
+};
+
+// (re)build the page at the stream position m.p (all lanes)
+__device__ __forceinline__ void gpage_build(WRng &m, GPage &pg, bool trig)
+{
+    wsync();   // earlier reads of the old page are done before it is overwritten
+    m.ensure(128);
+    pg.pb = m.p;
+    const double d = m.dbl(m.p + 2 * m.lane);
+    pg.d[m.lane] = d;
+    if (trig) {
+        const double a = d * CN_PI * 2;
+        pg.cs[m.lane] = cos(a);
+        pg.sn[m.lane] = sin(a);
+    }
+    wsync();
+}
+
+// One of the two goal-change loops at the end of CrowdSimDict.step:
 //   KIND 0  update_human_goals_randomly (crowd_sim.py:724-766): humans with v_pref != 0 draw U; if
 //           U <= goal_change_chance a new goal on the circle is rejection-sampled (angle, gx_noise, gy_noise);
 //   KIND 1  update_human_goal (crowd_sim.py:769-811): humans within their radius of the goal draw U; if
 //           U <= end_goal_change_chance radius / v_pref are jittered and create_agent_attributes'
 //           candidate is rejection-sampled.
-// Both walk the humans in index order. If every changing human accepts its FIRST try, the word position
-// of every draw is fixed: the walk becomes a table of U values (lane = (eligible human k, changes
-// before it c), one draw each) plus a scalar scan, and all first tries are tested at once, lane =
-// (changing human, agent), each against the goals the earlier humans then have. Up to the first human
-// whose first try is rejected this IS the sequential result; that human runs the ordinary rejection
-// loop (wave_reject2) and the walk resumes after it. `sp`: wave LDS scratch, 3*32 doubles.
+// Both walk the humans in index order, as the reference does, over a page of precomputed draws (GPage):
+// the walk itself is wave-uniform table reads; a changing human tests J tries at once, lane = (try t,
+// agent a), against the robot and the other humans (earlier humans already carry their new goals); the
+// first try without a hit wins. Bounded by max_tries like every rejection loop.
 template <int KIND>
-__device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, uint32_t &ovf, int sc, double *sp)
+__device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, uint32_t &ovf, int sc, double *sp,
+                                         int64_t edbg = -1)
 {
-    int dbg = 0;   // diagnostics: 1000 * rounds + eligible humans + 100 * changes
+#ifdef CN_STAMPS
+    unsigned long long tq = clock64(), t_walk = 0, t_first = 0, t_rej = 0;
+#define GP_LAP(acc) do { const unsigned long long t_ = clock64(); acc += t_ - tq; tq = t_; } while (0)
+#else
+#define GP_LAP(acc) do { } while (0)
+#endif
+    (void)sp;
+    int dbg = 0;   // diagnostics: 1000 * batches + eligible humans + 100 * changes
     const int N = c.human_num, lane = m.lane;
-    double *ngx = sp, *ngy = sp + 32, *nr = sp + 64;
     const double chance = KIND == 0 ? c.goal_change_chance : c.end_goal_change_chance;
     const int W = KIND == 0 ? 6 : cand_words(sc);
-    const int JW = KIND == 0 ? 0 : 2 * ((c.random_radii ? 1 : 0) + (c.random_v_pref ? 1 : 0));
-    const int SW = JW + W;     // words of one accepted-first-try change after its U
+    const bool trig = KIND == 0 || sc == CN_SC_CIRCLE_CROSSING;
     bool elig_l = false;       // eligibility reads only the human's own goal / radius: fixed up front
     if (lane < N) {
         if (KIND == 0) elig_l = en.hvp[lane] != 0;
         else elig_l = norm_lt(en.hgx[lane] - en.hpx[lane], en.hgy[lane] - en.hpy[lane], en.hr[lane]);
     }
-    const uint64_t elig = __ballot(elig_l);
-    dbg += __popcll(elig);
-    int i0 = 0;
-    while (i0 < N) {
-        const uint64_t rem = elig & (~0ull << i0);
-        if (!rem) break;
-        dbg += 1000;
-        const int n = __popcll(rem);
-        m.ensure(n * (2 + SW));
-        const int p0 = m.p;
-        // ---- walk: U of the k-th eligible human sits at p0 + 2k + SW*c, c = changes before it
-        uint64_t chg = 0;
-        int posl = -1, cnum = 0;
-        if (n * (n + 1) / 2 <= 64) {
-            int k = 0, cc = lane;
-            while (cc > k) { cc -= k + 1; ++k; }
-            const bool dec = lane < n * (n + 1) / 2 && m.dbl(p0 + 2 * k + SW * cc) <= chance;
-            const uint64_t B = __ballot(dec);
-            uint64_t mm = rem;
-            for (int kk = 0; kk < n; ++kk) {
-                const int h = __ffsll((long long)mm) - 1;
-                mm &= mm - 1;
-                if ((B >> (kk * (kk + 1) / 2 + cnum)) & 1ull) {
-                    chg |= 1ull << h;
-                    if (lane == h) posl = p0 + 2 * (kk + 1) + SW * cnum;
-                    ++cnum;
-                }
-            }
-        } else {
-            int p = p0;
-            for (int i = i0; i < N; ++i) {
-                if (!((rem >> i) & 1ull)) continue;
-                const double U = m.dbl(p);
-                p += 2;
-                if (U <= chance) {
-                    chg |= 1ull << i;
-                    if (lane == i) posl = p;
-                    p += SW;
-                    ++cnum;
-                }
+    uint64_t rem = __ballot(elig_l);
+    dbg += __popcll(rem);
+    if (!rem) return dbg;
+    GPage pg;
+    pg.d = m.sl; pg.cs = m.sl + 64; pg.sn = m.sl + 128;
+    gpage_build(m, pg, trig);
+    const int NA = N;              // robot + the other N-1 humans
+    const int JA = 64 / NA;        // tries per batch the lanes hold
+    const int JP = 128 / W;        // tries per batch a fresh page holds
+    GP_LAP(t_walk);
+    while (rem) {
+        const int h = __ffsll((long long)rem) - 1;
+        rem &= rem - 1;
+        if (m.p + 2 > pg.pb + 128) gpage_build(m, pg, trig);
+        const double U = pg.dbl(m.p);
+        m.p += 2;
+        if (!(U <= chance)) continue;
+        dbg += 100;
+        double r_self = en.hr[h], vpc = en.hvp[h];
+        if (KIND == 1) {
+            const int jw = 2 * ((c.random_radii ? 1 : 0) + (c.random_v_pref ? 1 : 0));
+            if (jw) {
+                if (m.p + jw > pg.pb + 128) gpage_build(m, pg, trig);
+                if (c.random_radii) { r_self += -0.1 + (0.1 - -0.1) * pg.dbl(m.p); m.p += 2; }
+                if (c.random_v_pref) { vpc += -0.1 + (0.1 - -0.1) * pg.dbl(m.p); m.p += 2; }
+                if (lane == 0) { en.hr[h] = r_self; en.hvp[h] = vpc; }
             }
         }
-        const int pend = p0 + 2 * n + SW * cnum;
-        if (!chg) { m.p = pend; break; }
-        dbg += 100 * __popcll(chg);
-        // ---- first tries: candidate per changing human (its lane), then lane = (candidate, agent)
-        const bool mine = lane < N && ((chg >> lane) & 1ull);
-        double r_i = 0, vp_i = 0;
-        if (mine) {
-            int q = posl;
-            double gx, gy;
-            r_i = en.hr[lane]; vp_i = en.hvp[lane];
-            if (KIND == 0) {
-                const double vp = en.hvp[lane] == 0 ? 1.0 : en.hvp[lane];
-                const double angle = m.dbl(q) * CN_PI * 2;
-                const double gxn = (m.dbl(q + 2) - 0.5) * vp, gyn = (m.dbl(q + 4) - 0.5) * vp;
-                gx = c.circle_radius * cos(angle) + gxn;
-                gy = c.circle_radius * sin(angle) + gyn;
-            } else {
-                if (c.random_radii) { r_i += -0.1 + (0.1 - -0.1) * m.dbl(q); q += 2; }
-                if (c.random_v_pref) { vp_i += -0.1 + (0.1 - -0.1) * m.dbl(q); q += 2; }
-                double px, py, hd, vpo;
-                cand_attributes(c, m, q, sc, vp_i, r_i, en.rr, px, py, gx, gy, hd, vpo);
-            }
-            ngx[lane] = gx; ngy[lane] = gy; nr[lane] = r_i;
-        }
-        wsync();
-        const int NA = N;                      // robot + the other N-1 humans
-        const int CPP = 64 / NA;               // candidates per pass
-        const int ncand = __popcll(chg);
-        int f = 64;
-        for (int c0 = 0; c0 < ncand && f == 64; c0 += CPP) {
-            const int ci = lane / NA, a = lane - ci * NA;
-            int h = -1;
-            if (ci < CPP && c0 + ci < ncand) {
-                uint64_t mm = chg;
-                for (int k = 0; k < c0 + ci; ++k) mm &= mm - 1;
-                h = __ffsll((long long)mm) - 1;
-            }
-            bool bad = false;
-            if (h >= 0) {
-                // agents: robot, then humans in order; earlier changing humans already carry new goals
-                double ax, ay, agx, agy, ar;
-                if (a == 0) { ax = en.rpx; ay = en.rpy; agx = en.rgx; agy = en.rgy; ar = en.rr; }
-                else {
-                    const int j = a - 1 < h ? a - 1 : a;
-                    ax = en.hpx[j]; ay = en.hpy[j];
-                    if (j < h && ((chg >> j) & 1ull)) { agx = ngx[j]; agy = ngy[j]; ar = nr[j]; }
-                    else { agx = en.hgx[j]; agy = en.hgy[j]; ar = en.hr[j]; }
+        const double vpk = (KIND == 0 && vpc == 0) ? 1.0 : vpc;
+        GP_LAP(t_walk);
+        for (int t0 = 0;; ) {
+            if (m.p + W * min(JA, JP) > pg.pb + 128) gpage_build(m, pg, trig);
+            const int J = min(min(JA, (pg.pb + 128 - m.p) / W), c.max_tries - t0);   // >= 1
+            const int t = lane / NA, a = lane - t * NA;
+            const bool valid = t < J;
+            double gx = 0, gy = 0;
+            bool bad = true;
+            if (valid) {
+                const int q = m.p + W * t;
+                if (KIND == 0) {
+                    gx = c.circle_radius * pg.cos2pi(q) + (pg.dbl(q + 2) - 0.5) * vpk;
+                    gy = c.circle_radius * pg.sin2pi(q) + (pg.dbl(q + 4) - 0.5) * vpk;
+                } else {
+                    double px, py, hd, vp;
+                    cand_attributes(c, pg, q, sc, vpc, r_self, en.rr, px, py, gx, gy, hd, vp);
                 }
-                const double md = nr[h] + ar + c.discomfort_dist;
-                bad = norm_lt(ngx[h] - ax, ngy[h] - ay, md) || norm_lt(ngx[h] - agx, ngy[h] - agy, md);
+                bad = goal_hit(c, en, h, r_self, gx, gy, a);
             }
+            dbg += 1000;
             const uint64_t badm = __ballot(bad);
             const uint64_t gmask = NA >= 64 ? ~0ull : ((1ull << NA) - 1ull);
-            for (int k = 0; k < CPP && c0 + k < ncand; ++k) {
-                if ((badm >> (k * NA)) & gmask) {
-                    uint64_t mm = chg;
-                    for (int q = 0; q < c0 + k; ++q) mm &= mm - 1;
-                    f = __ffsll((long long)mm) - 1;
-                    break;
-                }
+            int win = -1;
+            for (int k = 0; k < J; ++k)
+                if (((badm >> (k * NA)) & gmask) == 0) { win = k; break; }
+            if (win < 0 && t0 + J >= c.max_tries) { win = J - 1; ++ovf; }
+            if (win >= 0) {
+                if (lane == win * NA) { en.hgx[h] = gx; en.hgy[h] = gy; }   // the winning try's a = 0 lane
+                m.p += W * (win + 1);
+                wsync();
+                break;
             }
+            m.p += W * J;
+            t0 += J;
         }
-        if (mine && lane < f) {
-            en.hgx[lane] = ngx[lane]; en.hgy[lane] = ngy[lane];
-            if (KIND == 1) { en.hr[lane] = r_i; en.hvp[lane] = vp_i; }
-        }
-        wsync();
-        if (f == 64) { m.p = pend; break; }
-        // ---- human f rejected its first try: the ordinary rejection loop from that try on
-        const int qf = __shfl(posl, f);
-        const double rf = __shfl(r_i, f), vpf = __shfl(vp_i, f);
-        if (KIND == 1 && lane == 0) { en.hr[f] = rf; en.hvp[f] = vpf; }
-        wsync();
-        m.p = qf + JW;   // its candidate words follow the U draw and the radius / v_pref jitter draws
-        const double r_self = KIND == 1 ? rf : en.hr[f];
-        const double vpk0 = en.hvp[f] == 0 ? 1.0 : en.hvp[f];
-        const int tw = wave_reject2(m, W, NA, c.max_tries, ovf, [&](int q, int t) {
-            double gx, gy;
-            if (KIND == 0) {
-                const double angle = m.dbl(q) * CN_PI * 2;
-                const double gxn = (m.dbl(q + 2) - 0.5) * vpk0, gyn = (m.dbl(q + 4) - 0.5) * vpk0;
-                gx = c.circle_radius * cos(angle) + gxn;
-                gy = c.circle_radius * sin(angle) + gyn;
-            } else {
-                double px, py, hd, vp;
-                cand_attributes(c, m, q, sc, vpf, rf, en.rr, px, py, gx, gy, hd, vp);
-            }
-            m.sl[t] = gx; m.sl[64 + t] = gy;
-        }, [&](int t, int a) { return goal_hit(c, en, f, r_self, m.sl[t], m.sl[64 + t], a); });
-        if (lane == 0) { en.hgx[f] = m.sl[tw]; en.hgy[f] = m.sl[64 + tw]; }
-        wsync();
-        i0 = f + 1;
+        GP_LAP(t_first);
     }
+#ifdef CN_STAMPS
+    if (lane == 0 && edbg >= 0 && edbg < 8192) {
+        cn_stamp_b[edbg * CN_NSTAMP + 8 + 3 * KIND] = t_walk;
+        cn_stamp_b[edbg * CN_NSTAMP + 9 + 3 * KIND] = t_first;
+        cn_stamp_b[edbg * CN_NSTAMP + 10 + 3 * KIND] = t_rej;
+    }
+#endif
+#undef GP_LAP
+    (void)edbg;
     return dbg;
 }
 
@@ -1309,9 +1285,9 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
     wsync();
     STAMP_B(e, 1);
     int dbg0 = 0, dbg1 = 0;
-    if (rgoal) dbg0 = goal_pass<0>(c, en, m, ovf, sc, sp);
+    if (rgoal) dbg0 = goal_pass<0>(c, en, m, ovf, sc, sp, e);
     STAMP_B(e, 2);
-    if (egoal) dbg1 = goal_pass<1>(c, en, m, ovf, sc, sp);
+    if (egoal) dbg1 = goal_pass<1>(c, en, m, ovf, sc, sp, e);
     STAMP_B(e, 3);
 #ifdef CN_STAMPS
     if (lane == 0 && e < 8192) { cn_stamp_b[e * CN_NSTAMP + 6] = dbg0; cn_stamp_b[e * CN_NSTAMP + 7] = dbg1; }

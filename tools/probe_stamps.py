@@ -96,10 +96,13 @@ def run(variant, E=4096, N=10, steps=300):
             part = gg[:, 1] if slot == 6 else gg[:, 2]
             print("     %s pass: eligible mean %.2f, rounds mean %.2f max %d, changes (1st round) mean %.2f" % (
                 nm, elig.mean(), rounds.mean(), rounds.max(), chg.mean()))
+            k0 = 8 if slot == 6 else 11
             for r in range(int(rounds.max()) + 1):
                 sel = rounds == r
                 if sel.any():
-                    print("        %d rounds: %4d envs, cycles median %d max %d" % (r, sel.sum(), np.median(part[sel]), part[sel].max()))
+                    print("        %d rounds: %4d envs, cycles median %d max %d | walk %d first-tries %d reject-loop %d (mean)" % (
+                        r, sel.sum(), np.median(part[sel]), part[sel].max(), goal[sel, k0].mean(), goal[sel, k0 + 1].mean(),
+                        goal[sel, k0 + 2].mean()))
     eng.close()
 
 
