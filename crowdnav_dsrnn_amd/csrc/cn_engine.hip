@@ -1212,6 +1212,26 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
         const double vpk = (KIND == 0 && vpc == 0) ? 1.0 : vpc;
         GP_LAP(t_walk);
         for (int t0 = 0;; ) {
+            if (t0 > 0) {
+                // crowded (the first batch was all rejected): the remaining tries one per lane, 64 at a
+                // time, straight from the stream (wave_reject2); its try slots overwrite the page
+                const int tw = wave_reject2(m, W, NA, c.max_tries - t0, ovf, [&](int q, int tt) {
+                    double gx, gy;
+                    if (KIND == 0) {
+                        gx = c.circle_radius * m.cos2pi(q) + (m.dbl(q + 2) - 0.5) * vpk;
+                        gy = c.circle_radius * m.sin2pi(q) + (m.dbl(q + 4) - 0.5) * vpk;
+                    } else {
+                        double px, py, hd, vp;
+                        cand_attributes(c, m, q, sc, vpc, r_self, en.rr, px, py, gx, gy, hd, vp);
+                    }
+                    m.sl[tt] = gx; m.sl[64 + tt] = gy;
+                }, [&](int tt, int a) { return goal_hit(c, en, h, r_self, m.sl[tt], m.sl[64 + tt], a); });
+                if (lane == 0) { en.hgx[h] = m.sl[tw]; en.hgy[h] = m.sl[64 + tw]; }
+                wsync();
+                pg.pb = -(1 << 28);   // forces a rebuild before the next read
+                GP_LAP(t_rej);
+                break;
+            }
             if (m.p + W * min(JA, JP) > pg.pb + 128) gpage_build(m, pg, trig);
             const int J = min(min(JA, (pg.pb + 128 - m.p) / W), c.max_tries - t0);   // >= 1
             const int t = lane / NA, a = lane - t * NA;
