@@ -952,6 +952,60 @@ __device__ int wave_reject2(WRng &m, int W, int NA, int max_tries, uint32_t &ovf
     }
 }
 
+// Crowded goal rejection (a goal pass whose first batch was all rejected; in square_crossing at N = 25
+// most of these loops run to max_tries): one try per lane, 64 at a time, straight from the stream; the
+// agents (robot, then the other humans in index order) sit in an LDS table with their minimum distance
+// precomputed, and each lane tests them four at a time with the loads of a group issued together (the
+// agent-at-a-time loop was bound by dependent LDS latency). Same result as goal_hit over the tries in
+// order; returns the winning slot (m.sl[t], m.sl[64 + t]), m.p after its words.
+template <typename FC>
+__device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, int self, double r_self, int W,
+                                   int max_tries, uint32_t &ovf, FC cand)
+{
+    const int lane = m.lane, NA = c.human_num;
+    double *tx = m.sl + 128, *ty = tx + 32, *tgx = tx + 64, *tgy = tx + 96, *tmd = tx + 128;   // [32] each
+    if (lane < NA) {
+        double ar;
+        if (lane == 0) { tx[0] = en.rpx; ty[0] = en.rpy; tgx[0] = en.rgx; tgy[0] = en.rgy; ar = en.rr; }
+        else {
+            const int j = lane - 1 < self ? lane - 1 : lane;
+            tx[lane] = en.hpx[j]; ty[lane] = en.hpy[j]; tgx[lane] = en.hgx[j]; tgy[lane] = en.hgy[j]; ar = en.hr[j];
+        }
+        tmd[lane] = r_self + ar + c.discomfort_dist;
+    }
+    const int J = min(64, CN_MT_N / W);
+    for (int t0 = 0;; t0 += J) {
+        m.ensure(W * J);
+        const int nt = min(J, max_tries - t0);
+        double gx = 0, gy = 0;
+        if (lane < nt) {
+            cand(m.p + W * lane, lane);
+            gx = m.sl[lane]; gy = m.sl[64 + lane];
+        }
+        wsync();
+        bool bad = lane >= nt;
+        for (int a0 = 0; a0 < NA && !bad; a0 += 4) {
+            double x[4], y[4], u[4], v[4], d[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int a = min(a0 + k, NA - 1);   // a repeated last agent does not change the outcome
+                x[k] = tx[a]; y[k] = ty[a]; u[k] = tgx[a]; v[k] = tgy[a]; d[k] = tmd[a];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                bad = bad | norm_lt(gx - x[k], gy - y[k], d[k]) | norm_lt(gx - u[k], gy - v[k], d[k]);
+        }
+        const uint64_t okm = __ballot(!bad);
+        if (okm) {
+            const int first = __ffsll((long long)okm) - 1;
+            m.p += W * (first + 1);
+            return first;
+        }
+        if (t0 + nt >= max_tries) { m.p += W * nt; ++ovf; return nt - 1; }
+        m.p += W * J;
+        wsync();   // slots are rewritten by the next batch
+    }
+}
 
 // The random part of CrowdSimDict.reset (crowd_sim_dict.py:110-156; generate_robot_humans,
 // crowd_sim.py:555-663; generate_circle_crossing_human :359-393): reseed the env's stream with
@@ -1213,9 +1267,9 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
         GP_LAP(t_walk);
         for (int t0 = 0;; ) {
             if (t0 > 0) {
-                // crowded (the first batch was all rejected): the remaining tries one per lane, 64 at a
-                // time, straight from the stream (wave_reject2); its try slots overwrite the page
-                const int tw = wave_reject2(m, W, NA, c.max_tries - t0, ovf, [&](int q, int tt) {
+                // crowded (the first batch was all rejected): the remaining tries 64 candidates at a time
+                // straight from the stream (goal_reject_crowded); its try slots overwrite the page
+                const int tw = goal_reject_crowded(c, en, m, h, r_self, W, c.max_tries - t0, ovf, [&](int q, int tt) {
                     double gx, gy;
                     if (KIND == 0) {
                         gx = c.circle_radius * m.cos2pi(q) + (m.dbl(q + 2) - 0.5) * vpk;
@@ -1225,7 +1279,7 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
                         cand_attributes(c, m, q, sc, vpc, r_self, en.rr, px, py, gx, gy, hd, vp);
                     }
                     m.sl[tt] = gx; m.sl[64 + tt] = gy;
-                }, [&](int tt, int a) { return goal_hit(c, en, h, r_self, m.sl[tt], m.sl[64 + tt], a); });
+                });
                 if (lane == 0) { en.hgx[h] = m.sl[tw]; en.hgy[h] = m.sl[64 + tw]; }
                 wsync();
                 pg.pb = -(1 << 28);   // forces a rebuild before the next read
