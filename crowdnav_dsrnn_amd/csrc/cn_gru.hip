@@ -26,12 +26,14 @@ namespace {
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // gi, gh: [B][3H] (r | z | n blocks); hm: [B][H] the masked previous state; m_next: [B] or null;
-// h_out: [B][H]; hm_next: [B][H] or null (= h_out * m_next); save: [B][4H] (r | z | n | gh_n) or null.
+// h_out: [B][H]; hm_next: [B][H] or null (= h_out * m_next); save: [B][4H] (r | z | n | gh_n) or null;
+// h_out2: a second copy of h_out in a grouped row layout (row b at (b / g2) * ld2 + (b % g2) * H), or null.
 __global__ __launch_bounds__(256) void cn_gru_fwd_kernel(int64_t B, int H, const float *__restrict__ gi,
                                                          const float *__restrict__ gh,
                                                          const float *__restrict__ hm,
                                                          const float *__restrict__ m_next, float *__restrict__ h_out,
-                                                         float *__restrict__ hm_next, float *__restrict__ save)
+                                                         float *__restrict__ hm_next, float *__restrict__ save,
+                                                         float *__restrict__ h_out2, int64_t g2, int64_t ld2)
 {
     const int H4 = H >> 2;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -54,6 +56,7 @@ __global__ __launch_bounds__(256) void cn_gru_fwd_kernel(int64_t B, int H, const
     CN_GATE(x) CN_GATE(y) CN_GATE(z) CN_GATE(w)
 #undef CN_GATE
     *(float4 *)(h_out + b * H + j) = h;
+    if (h_out2) *(float4 *)(h_out2 + (b / g2) * ld2 + (b % g2) * H + j) = h;
     if (hm_next) {
         const float m = m_next ? m_next[b] : 1.0f;
         *(float4 *)(hm_next + b * H + j) = make_float4(h.x * m, h.y * m, h.z * m, h.w * m);
@@ -125,11 +128,20 @@ extern "C" {
 int cn_gru_fwd_step(void *stream, int64_t B, int H, const float *gi, const float *gh, const float *hm,
                     const float *m_next, float *h_out, float *hm_next, float *save)
 {
+    return cn_gru_fwd_step_scatter(stream, B, H, gi, gh, hm, m_next, h_out, hm_next, save, nullptr, 1, 0);
+}
+
+int cn_gru_fwd_step_scatter(void *stream, int64_t B, int H, const float *gi, const float *gh, const float *hm,
+                         const float *m_next, float *h_out, float *hm_next, float *save, float *h_out2, int64_t g2,
+                         int64_t ld2)
+{
     if (B <= 0 || H <= 0 || (H & 3)) return cn_set_error(CN_EINVAL, "cn_gru_fwd_step: B > 0 and H % 4 == 0 required");
     if (!gi || !gh || !hm || !h_out) return cn_set_error(CN_EINVAL, "cn_gru_fwd_step: null operand");
     if (B * (H / 4) > (int64_t)0xffffffff * 256) return cn_set_error(CN_EINVAL, "cn_gru_fwd_step: B too large");
+    if (h_out2 && (g2 <= 0 || ld2 < g2 * H || (ld2 & 3) || ((uintptr_t)h_out2 & 15)))
+        return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_scatter: g2 > 0, ld2 >= g2 * H, ld2 % 4 == 0, 16-byte aligned h_out2");
     hipLaunchKernelGGL(cn_gru_fwd_kernel, dim3(grid_for(B, H)), dim3(256), 0, (hipStream_t)stream, B, H, gi, gh,
-                       hm, m_next, h_out, hm_next, save);
+                       hm, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }

@@ -39,6 +39,7 @@ class RolloutTrainer:
                 self.rollouts.obs[k][0].copy_(obs[k])
         else:
             self.rollouts.obs[0].copy_(obs)
+        self.srnn = getattr(actor_critic, "srnn", False) and isinstance(self.rollouts, SRNNRolloutStorage)
         self.episode_returns = []
         self.env_steps = 0
 
@@ -50,7 +51,9 @@ class RolloutTrainer:
         for step in range(r.num_steps):
             obs_s = {k: v[step] for k, v in r.obs.items()} if isinstance(r.obs, dict) else r.obs[step]
             hxs_s = r.hidden(step)
-            value, action, logp, hxs = self.ac.act(obs_s, hxs_s, r.masks[step], deterministic=self.deterministic)
+            # the new recurrent state goes straight into the storage slot insert() would copy it to
+            value, action, logp, hxs = self.ac.act(obs_s, hxs_s, r.masks[step], deterministic=self.deterministic,
+                                                   **({"out_hxs": r.hidden_slot()} if self.srnn else {}))
             obs, reward, done, _, _, ep_ret, _ = self.envs.step_device(action)
             masks = (1.0 - done.float()).unsqueeze(1)
             r.insert(obs, hxs, action, logp, value, reward.unsqueeze(1), masks, torch.ones_like(masks))

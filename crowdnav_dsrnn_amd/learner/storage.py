@@ -59,7 +59,9 @@ class SRNNRolloutStorage:
             self.obs[k][s + 1].copy_(obs[k])
         hs = 1 if self.compact_hidden else s + 1
         for k in recurrent_hidden_states:
-            self.recurrent_hidden_states[k][hs].copy_(recurrent_hidden_states[k])
+            dst = self.recurrent_hidden_states[k][hs]
+            if recurrent_hidden_states[k].data_ptr() != dst.data_ptr():   # act(out_hxs=hidden_slot()) wrote it
+                dst.copy_(recurrent_hidden_states[k])
         self.actions[s].copy_(actions)
         self.action_log_probs[s].copy_(action_log_probs)
         self.value_preds[s].copy_(value_preds)
@@ -71,6 +73,11 @@ class SRNNRolloutStorage:
     def hidden(self, step):
         """The recurrent state act() consumes at `step` (recurrent_hidden_states[k][step] in train.py:227)."""
         i = (0 if step == 0 else 1) if self.compact_hidden else step
+        return {k: v[i] for k, v in self.recurrent_hidden_states.items()}
+
+    def hidden_slot(self):
+        """Where insert() puts the state produced at the current step (act's out_hxs target)."""
+        i = 1 if self.compact_hidden else self.step + 1
         return {k: v[i] for k, v in self.recurrent_hidden_states.items()}
 
     def after_update(self):

@@ -8,6 +8,8 @@ linear(...)         — nn.Linear with a split-K weight gradient (library GEMMs;
 attention_pool(...) — EdgeAttention's weighted sum of the spatial edge states (cn_attn_pool_*).
 masked_gru(...)     — the mask-segmented GRU of the three DSRNN RNNs over a (T, B) sequence
                       (cn_gru_fwd_step / cn_gru_bwd_step + library GEMMs), with its own backward.
+gru_infer_step(...) — one no-autograd step of the same GRU for act(): reads the state through strided views
+                      and writes the new state straight into the (B, N + 1, H) layout (cn_gru_fwd_step_scatter).
 """
 import torch
 
@@ -190,6 +192,38 @@ def masked_gru(x, h0, masks, w_ih, w_hh, b_ih, b_hh):
     if x.dtype != torch.float32 or w_hh.shape[1] % 4:
         raise ValueError("masked_gru: fp32 operands and a hidden size divisible by 4 required")
     return _MaskedGRU.apply(x, h0, masks, w_ih, w_hh, b_ih, b_hh)
+
+
+def gru_infer_step(x, h0, m, w_ih, w_hh, b_ih, b_hh, dest):
+    """One masked GRU step without autograd (the T = 1 inference path of srnn_model.py:52-104).
+
+    x (R, F); h0 (R', G, H) or (R, H), any strides with a unit last stride (e.g. a slice of the
+    (B, N + 1, H) edge-state tensor, R = R' * G); m (R') per group row; dest: a (R', G, H) view with
+    the same grouping, or None. h0 * m is formed in a contiguous buffer first, so dest may alias h0.
+    Returns the new state (R, H) contiguous; the kernel also writes it into dest (cn_gru_fwd_step_scatter)."""
+    if not x.is_cuda:
+        raise EdgeFeaturesUnavailable("gru_infer_step runs only through the HIP step kernels; tensors are on %s"
+                                      % x.device)
+    H = w_hh.shape[1]
+    h0g = h0 if h0.dim() == 3 else h0.unsqueeze(1)
+    Rg, G = h0g.shape[0], h0g.shape[1]
+    R = Rg * G
+    dev = x.device
+    hm = torch.empty((Rg, G, H), dtype=torch.float32, device=dev)
+    torch.mul(h0g, m.reshape(Rg, 1, 1), out=hm)
+    gi = torch.addmm(b_ih, _c(x).reshape(R, -1), w_ih.t())
+    gh = torch.addmm(b_hh, hm.view(R, H), w_hh.t())
+    out = torch.empty((R, H), dtype=torch.float32, device=dev)
+    d_ptr, ld = None, 0
+    if dest is not None:
+        dg = dest if dest.dim() == 3 else dest.unsqueeze(1)
+        if tuple(dg.shape) != (Rg, G, H) or dg.stride(2) != 1 or dg.stride(1) != H or dg.dtype != torch.float32:
+            raise ValueError("gru_infer_step: dest must be a float32 (R', G, H) view with rows of H contiguous")
+        d_ptr, ld = dg.data_ptr(), dg.stride(0)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().cn_gru_fwd_step_scatter(_stream(dev), R, H, gi.data_ptr(), gh.data_ptr(), hm.data_ptr(),
+                                                   None, out.data_ptr(), None, None, d_ptr, G, ld))
+    return out
 
 
 class _AttnPool(torch.autograd.Function):

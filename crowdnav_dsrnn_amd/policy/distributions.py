@@ -6,7 +6,22 @@ from .utils import AddBias, init
 
 
 class FixedNormal(torch.distributions.Normal):
-    """distributions.py:36-45: log_probs summed over action dims, mode = mean."""
+    """distributions.py:36-45: log_probs summed over action dims, mode = mean.
+
+    Built with validate_args=False: torch's default argument validation reduces loc / scale / the
+    actions to a host bool (three device->host synchronisations per act()); it only raises on NaN or
+    non-positive inputs and never changes a value."""
+
+    def __init__(self, loc, scale):
+        super().__init__(loc, scale, validate_args=False)
+
+    def sample(self, sample_shape=torch.Size()):
+        """loc + scale * N(0, 1): the draw torch.normal(loc, scale) makes, without its std >= 0 check
+        (a device min + host read per call)."""
+        shape = self._extended_shape(sample_shape)
+        with torch.no_grad():
+            eps = torch.randn(shape, dtype=self.loc.dtype, device=self.loc.device)
+            return eps * self.scale.expand(shape) + self.loc.expand(shape)
 
     def log_probs(self, actions):
         return super().log_prob(actions).sum(-1, keepdim=True)

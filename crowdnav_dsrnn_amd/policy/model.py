@@ -37,13 +37,14 @@ class Policy(nn.Module):
     def forward(self, inputs, rnn_hxs, masks):
         raise NotImplementedError
 
-    def _infer(self, inputs, rnn_hxs, masks):
+    def _infer(self, inputs, rnn_hxs, masks, out_hxs=None):
         if self.srnn:
-            return self.base(inputs, rnn_hxs, masks, infer=True)
+            return self.base(inputs, rnn_hxs, masks, infer=True, out_hxs=out_hxs)
         return self.base(inputs, rnn_hxs, masks)
 
-    def act(self, inputs, rnn_hxs, masks, deterministic=False):
-        value, actor_features, rnn_hxs = self._infer(inputs, rnn_hxs, masks)
+    def act(self, inputs, rnn_hxs, masks, deterministic=False, out_hxs=None):
+        """out_hxs (optional, srnn, no-grad): tensors that receive the new recurrent state (SRNN.forward)."""
+        value, actor_features, rnn_hxs = self._infer(inputs, rnn_hxs, masks, out_hxs)
         dist = self.dist(actor_features)
         action = dist.mode() if deterministic else dist.sample()
         action_log_probs = dist.log_probs(action)

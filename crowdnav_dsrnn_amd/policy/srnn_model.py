@@ -44,6 +44,12 @@ class RNNBase(nn.Module):
         g = self.gru
         return ops.masked_gru(x, h0, masks, g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0)
 
+    def infer_step(self, x, h0, m, dest):
+        """T = 1 without autograd: ops.gru_infer_step (new state also written into `dest`, which may be a
+        slice of the (B, N + 1, H) state tensor and may alias h0)."""
+        g = self.gru
+        return ops.gru_infer_step(x, h0, m, g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0, dest)
+
 
 class HumanNodeRNN(RNNBase):
     """Robot node RNN (srnn_model.py:109-173)."""
@@ -61,11 +67,15 @@ class HumanNodeRNN(RNNBase):
         self.edge_attention_embed = Linear(self.edge_rnn_size * 2, self.embedding_size)
         self.output_linear = Linear(self.rnn_size, self.output_size)
 
-    def forward(self, node_embed, h_temporal, h_spatial_other, h, masks):
-        """node_embed (T,B,64) = relu(encoder_linear(robot_linear(robot_node))) from the fused kernel."""
+    def forward(self, node_embed, h_temporal, h_spatial_other, h, masks, dest=None):
+        """node_embed (T,B,64) = relu(encoder_linear(robot_linear(robot_node))) from the fused kernel.
+        dest (B, 1, H) selects the no-autograd T = 1 path (the new state is written there)."""
         h_edges = torch.cat((h_temporal, h_spatial_other), -1)
         h_edges_embedded = self.relu(self.edge_attention_embed(h_edges))
         x = torch.cat((node_embed, h_edges_embedded), -1)
+        if dest is not None:
+            x = self.infer_step(x.reshape(-1, x.shape[-1]), h, masks.reshape(-1), dest)
+            return self.output_linear(x.unsqueeze(0)), dest
         x, h_new = self.masked_gru(x, h, masks)
         return self.output_linear(x), h_new
 
@@ -145,7 +155,12 @@ class SRNN(nn.Module):
         self.human_node_final_linear = init_(nn.Linear(self.output_size, 2))  # unused by forward (keys)
         self.num_edges = self.human_num + 1
 
-    def forward(self, inputs, rnn_hxs, masks, infer=False):
+    def forward(self, inputs, rnn_hxs, masks, infer=False, out_hxs=None):
+        """srnn_model.py:409-504. `out_hxs` (optional, inference only): preallocated
+        {'human_node_rnn': (B,1,128), 'human_human_edge_rnn': (B,N+1,256)} that receive the new state (they
+        may be the very tensors of rnn_hxs: the state is updated in place); rnn_hxs then holds them."""
+        if infer and not torch.is_grad_enabled():
+            return self._infer_step(inputs, rnn_hxs, masks, out_hxs)
         if infer:
             T, B = 1, self.nenv
         else:
@@ -177,3 +192,36 @@ class SRNN(nn.Module):
         if infer:
             return self.critic_linear(hidden_critic).squeeze(0), hidden_actor.squeeze(0), rnn_hxs
         return self.critic_linear(hidden_critic).view(-1, 1), hidden_actor.view(-1, self.output_size), rnn_hxs
+
+    def _infer_step(self, inputs, rnn_hxs, masks, out_hxs):
+        """The act() step without autograd: same arithmetic as the T = 1 path of forward(), but the GRUs
+        read the (B, N + 1, H) edge state through strided views and write the new state straight into its
+        destination (cn_gru_fwd_step_scatter) instead of slicing copies, a clone and a torch.cat."""
+        B = self.nenv
+        N = inputs["spatial_edges"].shape[-2]
+        te, se, ne = ops.edge_features(
+            inputs["robot_node"].reshape(B, 1, 7), inputs["temporal_edges"].reshape(B, 1, 2),
+            inputs["spatial_edges"].reshape(B, N, 2),
+            self.humanhumanEdgeRNN_temporal.encoder_linear.weight, self.humanhumanEdgeRNN_temporal.encoder_linear.bias,
+            self.humanhumanEdgeRNN_spatial.encoder_linear.weight, self.humanhumanEdgeRNN_spatial.encoder_linear.bias,
+            self.robot_linear.weight, self.robot_linear.bias,
+            self.humanNodeRNN.encoder_linear.weight, self.humanNodeRNN.encoder_linear.bias)
+        m = masks.reshape(B)
+        h_edge = rnn_hxs["human_human_edge_rnn"].reshape(B, self.num_edges, -1)
+        h_node = rnn_hxs["human_node_rnn"].reshape(B, 1, -1)
+        H = h_edge.shape[-1]
+        if out_hxs is None:
+            d_edge = torch.empty_like(h_edge)
+            d_node = torch.empty_like(h_node)
+        else:
+            d_edge = out_hxs["human_human_edge_rnn"].view(B, self.num_edges, H)
+            d_node = out_hxs["human_node_rnn"].view(B, 1, -1)
+        out_t = self.humanhumanEdgeRNN_temporal.infer_step(te.reshape(B, 64), h_edge[:, 0:1, :], m, d_edge[:, 0:1, :])
+        out_s = self.humanhumanEdgeRNN_spatial.infer_step(se.reshape(B * N, 64), h_edge[:, 1:, :], m, d_edge[:, 1:, :])
+        weighted, _ = self.attn(out_t.view(1, B, H), out_s.view(1, B, N, H))
+        outputs, _ = self.humanNodeRNN(ne.reshape(1, B, 64), out_t.view(1, B, H), weighted, h_node, m, dest=d_node)
+        rnn_hxs["human_node_rnn"] = d_node
+        rnn_hxs["human_human_edge_rnn"] = d_edge
+        hidden_critic = self.critic(outputs)
+        hidden_actor = self.actor(outputs)
+        return self.critic_linear(hidden_critic).squeeze(0), hidden_actor.squeeze(0), rnn_hxs

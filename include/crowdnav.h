@@ -199,6 +199,14 @@ int cn_edge_features(void *stream, int64_t E, int N,
  * save [B][4H] = r | z | n | gh_n for the backward (NULL = skip). H % 4 == 0. */
 int cn_gru_fwd_step(void *stream, int64_t B, int H, const float *gi, const float *gh, const float *hm,
                     const float *m_next, float *h_out, float *hm_next, float *save);
+/* cn_gru_fwd_step plus a second copy of the new state h_out, written in a grouped row layout: row b at
+ * h_out2 + (b / g2) * ld2 + (b % g2) * H (16-byte aligned, ld2 >= g2 * H, ld2 % 4 == 0). Lets the
+ * inference step write the temporal (g2 = 1) and spatial (g2 = N) edge states straight into the
+ * reference's (B, N + 1, H) 'human_human_edge_rnn' layout (srnn_model.py:406-407, 450, 460) instead of
+ * a torch.cat + copy; h_out2 = NULL is cn_gru_fwd_step. */
+int cn_gru_fwd_step_scatter(void *stream, int64_t B, int H, const float *gi, const float *gh, const float *hm,
+                         const float *m_next, float *h_out, float *hm_next, float *save, float *h_out2, int64_t g2,
+                         int64_t ld2);
 
 /* Gradient of one step. In: acc [B][H] = dL/dhm of the later step (or dL/dh_T at the last step, with
  * m_next = NULL), m_next [B] that later step's mask, dout [B][H] = dL/dh_t from the outputs (NULL = 0),

@@ -223,6 +223,20 @@ def masked_gru_ref(x, h0, masks, w_ih, w_hh, b_ih, b_hh):
     return torch.stack(outs, 0), h
 
 
+def gru_infer_step_ref(x, h0, m, w_ih, w_hh, b_ih, b_hh, dest):
+    """Plain PyTorch restatement of ops.gru_infer_step: one masked GRU cell step over grouped rows,
+    the new state also written into dest."""
+    import torch
+
+    h0g = h0 if h0.dim() == 3 else h0.unsqueeze(1)
+    R, G, H = h0g.shape
+    hm = (h0g * m.reshape(R, 1, 1)).reshape(R * G, H)
+    h = torch.gru_cell(x.reshape(R * G, -1), hm, w_ih, w_hh, b_ih, b_hh)
+    if dest is not None:
+        (dest if dest.dim() == 3 else dest.unsqueeze(1)).copy_(h.view(R, G, H))
+    return h
+
+
 def attention_pool_ref(hs, attn):
     """Plain PyTorch restatement of EdgeAttention's weighted sum (srnn_model.py:320-333)."""
     import torch

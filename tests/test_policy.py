@@ -10,7 +10,8 @@ import numpy as np
 import pytest
 import torch
 
-from tests.helpers import attention_pool_ref, edge_features_fp32, masked_gru_ref, load, make_policy
+from tests.helpers import (attention_pool_ref, edge_features_fp32, gru_infer_step_ref, masked_gru_ref, load,
+                           make_policy)
 
 ATOL, RTOL = 2e-5, 1e-4
 
@@ -24,13 +25,22 @@ def _obs(d, p, dev):
     return {k: torch.from_numpy(d[p + k]).to(dev) for k in ("robot_node", "temporal_edges", "spatial_edges")}
 
 
-def _run_act(d, N, dev):
+def _run_act(d, N, dev, in_place=False, grad=False):
+    """act() on the fixture; in_place: the new state is written over the input state tensors
+    (out_hxs = rnn_hxs, the rollout loop's storage slot); grad: the autograd T = 1 path."""
     pol = make_policy(N, device=dev)
     p = "N%d_act_" % N
     obs = _obs(d, p + "obs_", dev)
     hxs = {k: torch.from_numpy(d[p + "hxs_" + k].copy()).to(dev) for k in ("human_node_rnn", "human_human_edge_rnn")}
+    masks = torch.from_numpy(d[p + "masks"]).to(dev)
+    if grad:
+        v, a, lp, nh = pol.act(obs, hxs, masks, deterministic=True)
+        return v.detach(), a.detach(), lp.detach(), {k: t.detach() for k, t in nh.items()}
     with torch.no_grad():
-        v, a, lp, nh = pol.act(obs, hxs, torch.from_numpy(d[p + "masks"]).to(dev), deterministic=True)
+        out = dict(hxs) if in_place else None
+        v, a, lp, nh = pol.act(obs, hxs, masks, deterministic=True, out_hxs=out)
+        if in_place:
+            assert all(nh[k].data_ptr() == out[k].data_ptr() for k in out)
     return v, a, lp, nh
 
 
@@ -89,8 +99,12 @@ def test_policy_graph_cpu_with_fp32_input_layers(dsrnn, N, monkeypatch):
 
     monkeypatch.setattr(ops, "edge_features", edge_features_fp32)
     monkeypatch.setattr(ops, "masked_gru", masked_gru_ref)
+    monkeypatch.setattr(ops, "gru_infer_step", gru_infer_step_ref)
     monkeypatch.setattr(ops, "attention_pool", attention_pool_ref)
     _check_act(dsrnn, N, _run_act(dsrnn, N, "cpu"))
+    _check_act(dsrnn, N, _run_act(dsrnn, N, "cpu", in_place=True))
+    with torch.enable_grad():   # the autograd (training-graph) T = 1 path
+        _check_act(dsrnn, N, _run_act(dsrnn, N, "cpu", grad=True))
     _check_eval(dsrnn, N, _run_eval(dsrnn, N, "cpu"))
 
 
@@ -98,6 +112,9 @@ def test_policy_graph_cpu_with_fp32_input_layers(dsrnn, N, monkeypatch):
 @pytest.mark.parametrize("N", [5, 10])
 def test_policy_act_gpu(dsrnn, N):
     _check_act(dsrnn, N, _run_act(dsrnn, N, "cuda:0"))
+    _check_act(dsrnn, N, _run_act(dsrnn, N, "cuda:0", in_place=True))
+    with torch.enable_grad():
+        _check_act(dsrnn, N, _run_act(dsrnn, N, "cuda:0", grad=True))
 
 
 @pytest.mark.gpu
