@@ -286,26 +286,106 @@ __device__ inline void norm_zone(double px, double py, double vx, double vy, dou
 __constant__ double c_circ_cos[64];
 __constant__ double c_circ_sin[64];
 
-__device__ inline bool disc_quad_intersect(double px, double py, double r, const double *qx, const double *qy)
+// GEOS's 64-gon buffer of the robot disc (Point.buffer(r)): vertex k at angle -k*pi/32
+__device__ __forceinline__ double gon_x(double px, double r, int k)
 {
-    // vertices recomputed on the fly (no 64-entry arrays: keeps the step kernel's VGPR budget)
-    auto VX = [&](int k) { return k == 0 ? px + r : px + r * c_circ_cos[k]; };
-    auto VY = [&](int k) { return k == 0 ? py : py + r * c_circ_sin[k]; };
-    for (int p = 0; p < 2; ++p) {
-        const int nv = p ? 64 : 4;
-        for (int k = 0; k < nv; ++k) {
-            const int k1 = (k + 1) % nv;
-            const double ex = p ? VX(k1) - VX(k) : qx[k1] - qx[k];
-            const double ey = p ? VY(k1) - VY(k) : qy[k1] - qy[k];
-            if (ex == 0.0 && ey == 0.0) continue;
-            const double nx = -ey, ny = ex;
-            double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
-            for (int v = 0; v < 64; ++v) { const double t = VX(v) * nx + VY(v) * ny; amin = t < amin ? t : amin; amax = t > amax ? t : amax; }
-            for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
-            if (amax < bmin || bmax < amin) return false;
-        }
+    k &= 63;
+    return k == 0 ? px + r : px + r * c_circ_cos[k];
+}
+__device__ __forceinline__ double gon_y(double py, double r, int k)
+{
+    k &= 63;
+    return k == 0 ? py : py + r * c_circ_sin[k];
+}
+
+// Extents of the 64-gon on axis n: the vertex projections V_k.n = P.n + r|n|cos(theta_k - phi) peak at
+// the vertex nearest phi (kmax) and bottom out opposite (kmax + 32); vertices two or more steps away
+// are smaller by >= ~r|n|*pi^2/1024 relative to the extreme, ~10^12 times any rounding of a projection,
+// so the extremes over a +-2 window equal those over all 64 vertices exactly (min / max are
+// order-independent).
+__device__ __forceinline__ void gon_extent(double px, double py, double r, double nx, double ny, int kmax,
+                                           double &amin, double &amax)
+{
+    amin = INFINITY; amax = -INFINITY;
+#pragma unroll
+    for (int d = -2; d <= 2; ++d) {
+        const double t = gon_x(px, r, kmax + d) * nx + gon_y(py, r, kmax + d) * ny;
+        const double u = gon_x(px, r, kmax + 32 + d) * nx + gon_y(py, r, kmax + 32 + d) * ny;
+        amax = t > amax ? t : amax;
+        amin = u < amin ? u : amin;
+    }
+}
+
+// Separating-axis test over the edge normals of the quad and of the 64-gon (the predicate the oracle,
+// oracle/cpu_ref.c:disc_quad_intersect, evaluates with all 64 vertices per axis): identical boolean.
+__device__ __forceinline__ bool disc_quad_sat(double px, double py, double r, const double *qx, const double *qy)
+{
+    const double step = CN_PI / 32;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // quad edges: the 64-gon's extreme vertex from the axis angle
+        const int k1 = (k + 1) & 3;
+        const double ex = qx[k1] - qx[k], ey = qy[k1] - qy[k];
+        if (ex == 0.0 && ey == 0.0) continue;
+        const double nx = -ey, ny = ex;
+        const int kmax = ((int)rint(-atan2(ny, nx) / step) % 64 + 64) % 64;
+        double amin, amax, bmin = INFINITY, bmax = -INFINITY;
+        gon_extent(px, py, r, nx, ny, kmax, amin, amax);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
+        if (amax < bmin || bmax < amin) return false;
+    }
+    for (int k = 0; k < 64; ++k) {  // 64-gon edge k -> k+1: its normal (-ey, ex) points at angle -(k + 1/2) pi/32
+        const double ex = gon_x(px, r, k + 1) - gon_x(px, r, k), ey = gon_y(py, r, k + 1) - gon_y(py, r, k);
+        if (ex == 0.0 && ey == 0.0) continue;
+        const double nx = -ey, ny = ex;
+        double amin, amax, bmin = INFINITY, bmax = -INFINITY;
+        gon_extent(px, py, r, nx, ny, k, amin, amax);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
+        if (amax < bmin || bmax < amin) return false;
     }
     return true;
+}
+
+// robot 64-gon vs a norm-zone quad (Point.buffer(r).intersects(zone), crowd_sim.py norm-zone penalty).
+// Away from the boundary the answer is geometric: the 64-gon lies between the discs of radius
+// r cos(pi/64) and r about P, so a centre distance to the (convex) quad below r cos(pi/64) - eps means
+// intersecting and above r + eps disjoint (eps = 1e-9 >> rounding of the inputs); only the thin band in
+// between runs the separating-axis test.
+__device__ __forceinline__ bool disc_quad_intersect(double px, double py, double r, const double *qx, const double *qy)
+{
+    const double eps = 1e-9;
+    double area2 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) area2 += qx[k] * qy[(k + 1) & 3] - qx[(k + 1) & 3] * qy[k];
+    int cls = -1;   // 1 / 0 decided by the distance classification, -1: the separating-axis test decides
+    if (fabs(area2) > 1e-12 && r > 1e-6) cls = disc_quad_classify(px, py, r, qx, qy, area2 > 0 ? 1.0 : -1.0, eps);
+    return cls >= 0 ? cls != 0 : disc_quad_sat(px, py, r, qx, qy);
+}
+
+__device__ __forceinline__ int disc_quad_classify(double px, double py, double r, const double *qx, const double *qy,
+                                                  double sgn, double eps)
+{
+    bool inside = true;
+    double d2 = INFINITY;   // squared distance from P to the quad's boundary segments
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int k1 = (k + 1) & 3;
+        const double ex = qx[k1] - qx[k], ey = qy[k1] - qy[k];
+        const double wx = px - qx[k], wy = py - qy[k];
+        if (sgn * (ex * wy - ey * wx) < 0) inside = false;
+        const double ee = ex * ex + ey * ey;
+        double t = ee > 0 ? (wx * ex + wy * ey) / ee : 0.0;
+        t = t < 0 ? 0 : (t > 1 ? 1 : t);
+        const double dx = wx - t * ex, dy = wy - t * ey;
+        const double dd = dx * dx + dy * dy;
+        d2 = dd < d2 ? dd : d2;
+    }
+    if (inside) return 1;
+    const double d = sqrt(d2);
+    if (d < r * 0.99879545620517241 - eps) return 1;   // cos(pi/64)
+    if (d > r + eps) return 0;
+    return -1;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2565,6 +2645,16 @@ int cn_set_error(int code, const char *msg) { return set_err(code, "%s", msg); }
         if (_e != hipSuccess) return set_err(CN_EHIP, "HIP error: %s", hipGetErrorString(_e)); \
     } while (0)
 
+__global__ void __launch_bounds__(64) cn_disc_quad_kernel(int64_t n, int mode, const double *px, const double *py,
+                                                          const double *r, const double *qx, const double *qy,
+                                                          int32_t *out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = mode ? disc_quad_sat(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i)
+                  : disc_quad_intersect(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i);
+}
+
 extern "C" {
 
 const char *cn_last_error(void) { return g_err; }
@@ -2873,6 +2963,16 @@ int cn_lidar_obs(cn_engine *g, void *stream, const uint8_t *reset_mask, int enab
     hipLaunchKernelGGL(cn_lidar_obs_kernel, dim3((unsigned)((g->E + 3) / 4)), dim3(256), 0, (hipStream_t)stream, g->s,
                        g->E, g->N, 0.5 * g->c.square_width, reset_mask, enable, beams, max_range, robot_radius,
                        lidar, obs);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
+
+int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, const double *py, const double *r,
+                       const double *qx, const double *qy, int32_t *out)
+{
+    if (n <= 0 || !px || !py || !r || !qx || !qy || !out) return set_err(CN_EINVAL, "cn_debug_disc_quad: n > 0 and buffers required");
+    hipLaunchKernelGGL(cn_disc_quad_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, n, mode,
+                       px, py, r, qx, qy, out);
     HIPCHK(hipGetLastError());
     return CN_OK;
 }

@@ -227,6 +227,13 @@ int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_n
 int cn_lidar_obs(cn_engine *eng, void *stream, const uint8_t *reset_mask, int enable, int beams, double max_range,
                  double robot_radius, float *lidar, float *obs);
 
+/* Test hook: the norm-zone predicate of the step kernel, robot 64-gon (GEOS Point.buffer(r)) vs convex quad
+ * (crowd_sim.py norm-zone penalty), for n cases on the device: px, py, r [n], qx, qy [n][4],
+ * out [n] (1 = intersecting). mode 0: the kernel's function (classification + separating axes), mode 1:
+ * the separating-axis test alone. Checked against oracle/cpu_ref.c:disc_quad_intersect in tests/. */
+int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, const double *py, const double *r,
+                       const double *qx, const double *qy, int32_t *out);
+
 /* out[r][h] = sum_n hs[r][n][h] * attn[r][n]; hs [R][N][H], attn [R][N], out [R][H]; H % 4 == 0. */
 int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, float *out);
 

@@ -729,6 +729,13 @@ static int disc_quad_intersect(double px, double py, double r, const double *qx,
     return 1;
 }
 
+/* test hook: the predicate above on n cases (tests/test_norm_zone.py checks the GPU's against it) */
+EXPORT void cnref_disc_quad(int64_t n, const double *px, const double *py, const double *r, const double *qx,
+                            const double *qy, int32_t *out)
+{
+    for (int64_t i = 0; i < n; ++i) out[i] = disc_quad_intersect(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i);
+}
+
 /* ------------------------------------------------------------------------------------------------ */
 /* spawn (crowd_sim.py:296-393, 555-663)                                                             */
 /* ------------------------------------------------------------------------------------------------ */

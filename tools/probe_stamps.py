@@ -34,6 +34,21 @@ def run(variant, E=4096, N=10, steps=300):
         c.sim.train_val_sim = ["square_crossing"]
         c.action_space.kinematics = "holonomic"
         c.robot.FOV = c.humans.FOV = 1.0
+    if variant in ("c5a", "c5b", "c5a_nonorm", "c5b_nonorm"):   # the two C5 engines (bench.engines_for)
+        c.humans.policy = "orca"
+        c.action_space.kinematics = "holonomic"
+        c.reward.norm_zones = not variant.endswith("nonorm")
+        if variant.startswith("c5a"):
+            N = 5
+            c.sim.train_val_sim = c.sim.test_sim = ["parallel_traffic", "perpendicular_traffic"]
+        else:
+            N = 1
+            c.sim.train_val_sim = c.sim.test_sim = ["side_pref_passing", "side_pref_overtaking", "side_pref_crossing"]
+            c.test.side_preference = True
+            c.sim.circle_radius = 4
+            c.humans.random_goal_changing = False
+            c.humans.end_goal_changing = False
+        c.sim.human_num = N
     eng = CrowdNavEngine(make_cn_config(c, num_envs=E), "cuda:0")
     eng.reset()
     L = _lib.lib()
