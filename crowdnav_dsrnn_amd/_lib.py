@@ -18,6 +18,28 @@ class NativeLibraryMissing(RuntimeError):
     pass
 
 
+class StaleNativeLibrary(NativeLibraryMissing):
+    """The library on disk was not built from the sources on disk (embedded CN_SRC_HASH differs)."""
+
+
+def _check_provenance(L):
+    """cn_version() carries the sha256 of the sources the library was built from (build.py). When the
+    sources are present (always in-tree, on the GPU box too) they must hash to the same value."""
+    from . import build
+
+    ver = L.cn_version().decode()
+    mark = build.HASH_MARK.decode()
+    got = ver.split(mark, 1)[1][:64] if mark in ver else None
+    if os.environ.get("CN_LIB_PATH") or not all(os.path.exists(d) for d in build.DEPS):
+        return ver
+    want = build.source_hash()
+    if got != want:
+        raise StaleNativeLibrary(
+            "%s was built from other sources (embedded %s, sources on disk %s): rebuild with "
+            "`python -m crowdnav_dsrnn_amd.build`" % (LIB_PATH, got, want))
+    return ver
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -30,6 +52,7 @@ def lib():
     cfgp = ctypes.POINTER(abi.CnConfig)
     L.cn_last_error.restype = ctypes.c_char_p
     L.cn_version.restype = ctypes.c_char_p
+    _check_provenance(L)
     L.cn_config_validate.argtypes = [cfgp]
     L.cn_create.argtypes = [cfgp, ctypes.c_int, ctypes.POINTER(vp)]
     L.cn_destroy.argtypes = [vp]

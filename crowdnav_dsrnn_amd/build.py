@@ -1,4 +1,10 @@
-"""Build the native library in-tree: crowdnav_dsrnn_amd/lib/libcrowdnav_hip.so (gfx950)."""
+"""Build the native library in-tree: crowdnav_dsrnn_amd/lib/libcrowdnav_hip.so (gfx950).
+
+Provenance: the library embeds `CN_SRC_HASH=<sha256 of the compile flags + every source it depends on>`
+(returned by cn_version()). `_lib.lib()` refuses a library whose embedded hash differs from the hash of
+the sources on disk, so a stale prebuilt binary can never stand in for the committed code.
+"""
+import hashlib
 import os
 import subprocess
 import sys
@@ -20,11 +26,37 @@ def hipcc():
     raise RuntimeError("hipcc not found")
 
 
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wno-unused-result"]
+HASH_MARK = b"CN_SRC_HASH="
+
+
+def source_hash():
+    """sha256 over the target arch, the compile flags and the bytes of every dependency, in order."""
+    h = hashlib.sha256()
+    h.update(("%s|%s|" % (ARCH, " ".join(FLAGS))).encode())
+    for d in DEPS:
+        h.update(os.path.relpath(d, REPO).encode() + b"\0")
+        with open(d, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def built_hash(path=LIB_PATH):
+    """The source hash embedded in a built library (None if absent or unreadable)."""
+    try:
+        with open(path, "rb") as f:
+            blob = f.read()
+    except OSError:
+        return None
+    i = blob.find(HASH_MARK)
+    if i < 0:
+        return None
+    return blob[i + len(HASH_MARK):i + len(HASH_MARK) + 64].decode("ascii", "replace")
+
+
 def needs_build():
-    if not os.path.exists(LIB_PATH):
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(d) > t for d in DEPS)
+    return built_hash() != source_hash()
 
 
 def build(force=False, verbose=False):
@@ -32,8 +64,7 @@ def build(force=False, verbose=False):
         return LIB_PATH
     os.makedirs(LIB_DIR, exist_ok=True)
     tmp = LIB_PATH + ".tmp%d" % os.getpid()
-    cmd = [hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-           "-Wno-unused-result", "-o", tmp] + SOURCES
+    cmd = [hipcc(), "--offload-arch=" + ARCH] + FLAGS + ['-DCN_SRC_HASH="%s"' % source_hash(), "-o", tmp] + SOURCES
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -347,22 +347,6 @@ __device__ __forceinline__ bool disc_quad_sat(double px, double py, double r, co
     return true;
 }
 
-// robot 64-gon vs a norm-zone quad (Point.buffer(r).intersects(zone), crowd_sim.py norm-zone penalty).
-// Away from the boundary the answer is geometric: the 64-gon lies between the discs of radius
-// r cos(pi/64) and r about P, so a centre distance to the (convex) quad below r cos(pi/64) - eps means
-// intersecting and above r + eps disjoint (eps = 1e-9 >> rounding of the inputs); only the thin band in
-// between runs the separating-axis test.
-__device__ __forceinline__ bool disc_quad_intersect(double px, double py, double r, const double *qx, const double *qy)
-{
-    const double eps = 1e-9;
-    double area2 = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) area2 += qx[k] * qy[(k + 1) & 3] - qx[(k + 1) & 3] * qy[k];
-    int cls = -1;   // 1 / 0 decided by the distance classification, -1: the separating-axis test decides
-    if (fabs(area2) > 1e-12 && r > 1e-6) cls = disc_quad_classify(px, py, r, qx, qy, area2 > 0 ? 1.0 : -1.0, eps);
-    return cls >= 0 ? cls != 0 : disc_quad_sat(px, py, r, qx, qy);
-}
-
 __device__ __forceinline__ int disc_quad_classify(double px, double py, double r, const double *qx, const double *qy,
                                                   double sgn, double eps)
 {
@@ -386,6 +370,22 @@ __device__ __forceinline__ int disc_quad_classify(double px, double py, double r
     if (d < r * 0.99879545620517241 - eps) return 1;   // cos(pi/64)
     if (d > r + eps) return 0;
     return -1;
+}
+
+// robot 64-gon vs a norm-zone quad (Point.buffer(r).intersects(zone), crowd_sim.py norm-zone penalty).
+// Away from the boundary the answer is geometric: the 64-gon lies between the discs of radius
+// r cos(pi/64) and r about P, so a centre distance to the (convex) quad below r cos(pi/64) - eps means
+// intersecting and above r + eps disjoint (eps = 1e-9 >> rounding of the inputs); only the thin band in
+// between runs the separating-axis test.
+__device__ __forceinline__ bool disc_quad_intersect(double px, double py, double r, const double *qx, const double *qy)
+{
+    const double eps = 1e-9;
+    double area2 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) area2 += qx[k] * qy[(k + 1) & 3] - qx[(k + 1) & 3] * qy[k];
+    int cls = -1;   // 1 / 0 decided by the distance classification, -1: the separating-axis test decides
+    if (fabs(area2) > 1e-12 && r > 1e-6) cls = disc_quad_classify(px, py, r, qx, qy, area2 > 0 ? 1.0 : -1.0, eps);
+    return cls >= 0 ? cls != 0 : disc_quad_sat(px, py, r, qx, qy);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2658,7 +2658,11 @@ __global__ void __launch_bounds__(64) cn_disc_quad_kernel(int64_t n, int mode, c
 extern "C" {
 
 const char *cn_last_error(void) { return g_err; }
-const char *cn_version(void) { return "crowdnav_dsrnn_amd 0.1 (gfx950)"; }
+#ifndef CN_SRC_HASH
+#define CN_SRC_HASH "unversioned"
+#endif
+// build.py passes the sha256 of the flags + sources; _lib.lib() compares it with the sources on disk
+const char *cn_version(void) { return "crowdnav_dsrnn_amd 0.2 (gfx950) CN_SRC_HASH=" CN_SRC_HASH; }
 
 int cn_config_validate(const cn_config *c)
 {

@@ -89,3 +89,14 @@ def test_make_cn_config_defaults_follow_make_env():
     c1 = make_cn_config(clone_config(Config()), num_envs=1)
     assert c1.phase == abi.PHASE_TEST
     assert abs(c.robot_fov - 2 * 3.141592653589793) < 1e-12
+
+
+def test_library_built_from_sources_on_disk(L):
+    """The loaded library embeds the sha256 of the sources it was built from (build.py) and it equals
+    the hash of the committed sources: GPU evidence produced with it belongs to this tree."""
+    from crowdnav_dsrnn_amd import build
+
+    ver = L.cn_version().decode()
+    assert "CN_SRC_HASH=" + build.source_hash() in ver
+    assert build.built_hash() == build.source_hash()
+    assert not build.needs_build()
