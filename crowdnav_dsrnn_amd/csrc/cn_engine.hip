@@ -388,70 +388,26 @@ __device__ __forceinline__ bool disc_quad_intersect(double px, double py, double
     return cls >= 0 ? cls != 0 : disc_quad_sat(px, py, r, qx, qy);
 }
 
+// crowd_sim.py:918-926,957-960 (norm zones on): both zones are built around the robot and
+// tested against its own disc. Out of line: the 64-gon separating-axis test would otherwise raise the
+// step kernel's register pressure (and scratch) for every workload, norm zones on or off.
+__device__ __noinline__ bool robot_norm_zone_violation(double px, double py, double vx, double vy, double rr, bool f32,
+                                                       int lhs)
+{
+    double zx[4], zy[4];
+    for (int z = 0; z < 2; ++z) {
+        norm_zone(px, py, vx, vy, rr, f32, lhs, z == 0, zx, zy);
+        if (disc_quad_intersect(px, py, rr, zx, zy)) return true;
+    }
+    return false;
+}
+
 // ------------------------------------------------------------------------------------------------
 // RVO2 v2.0 agent-0 solve (float32) with ORCA lines in LDS ([line][lane] float4: point.xy, dir.xy)
 // ------------------------------------------------------------------------------------------------
 #define RVO_EPSILON 0.00001f
 
-struct LineView {
-    float4 *base;
-    int tid, T;
-    __device__ float4 operator[](int k) const { return base[k * T + tid]; }
-    __device__ void set(int k, float4 v) const { base[k * T + tid] = v; }
-};
-
 __device__ inline float det2(float ax, float ay, float bx, float by) { return ax * by - ay * bx; }
-
-// linearProgram1 on plain lines
-__device__ bool lp1(const LineView &L, int no, float radius, float ox, float oy, bool dirOpt, float &rx, float &ry)
-{
-    const float4 ln = L[no];
-    const float dot = ln.x * ln.z + ln.y * ln.w;
-    const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
-    if (disc < 0.0f) return false;
-    const float sd = fsqrt(disc);
-    float tL = -dot - sd, tR = -dot + sd;
-    for (int i = 0; i < no; ++i) {
-        const float4 li = L[i];
-        const float den = det2(ln.z, ln.w, li.z, li.w);
-        const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
-        if (fabsf(den) <= RVO_EPSILON) {
-            if (num < 0.0f) return false;
-            continue;
-        }
-        const float t = fdiv(num, den);
-        if (den >= 0.0f) tR = (t < tR) ? t : tR;
-        else tL = (tL < t) ? t : tL;
-        if (tL > tR) return false;
-    }
-    if (dirOpt) {
-        if (ox * ln.z + oy * ln.w > 0.0f) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
-        else { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
-    } else {
-        const float t = ln.z * (ox - ln.x) + ln.w * (oy - ln.y);
-        if (t < tL) { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
-        else if (t > tR) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
-        else { rx = ln.x + t * ln.z; ry = ln.y + t * ln.w; }
-    }
-    return true;
-}
-
-__device__ int lp2(const LineView &L, int n, float radius, float ox, float oy, float &rx, float &ry, bool dirOpt = false)
-{
-    if (dirOpt) { rx = ox * radius; ry = oy * radius; }
-    else if (ox * ox + oy * oy > radius * radius) {
-        const float inv = fdiv(1.0f, fsqrt(ox * ox + oy * oy));
-        rx = (ox * inv) * radius; ry = (oy * inv) * radius;
-    } else { rx = ox; ry = oy; }
-    for (int i = 0; i < n; ++i) {
-        const float4 li = L[i];
-        if (det2(li.z, li.w, li.x - rx, li.y - ry) > 0.0f) {
-            const float tx = rx, ty = ry;
-            if (!lp1(L, i, radius, ox, oy, dirOpt, rx, ry)) { rx = tx; ry = ty; return i; }
-        }
-    }
-    return n;
-}
 
 // projected line of LP3's line li against lj (`valid` false when RVO2 skips it: parallel, same direction)
 __device__ __forceinline__ float4 proj_line(const float4 li, const float4 lj, bool &valid)
@@ -472,149 +428,6 @@ __device__ __forceinline__ float4 proj_line(const float4 li, const float4 lj, bo
     const float inv = fdiv(1.0f, fsqrt(ddx * ddx + ddy * ddy));
     r.z = ddx * inv; r.w = ddy * inv;
     return r;
-}
-
-// linearProgram3 (numObstLines = 0); projected lines stored once per violating line in `PL`
-__device__ void lp3(const LineView &L, const LineView &PL, int n, int begin, float radius, float &rx, float &ry)
-{
-    float distance = 0.0f;
-    for (int i = begin; i < n; ++i) {
-        const float4 li = L[i];
-        if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
-            int np = 0;
-            for (int j = 0; j < i; ++j) {
-                bool v;
-                const float4 pj = proj_line(li, L[j], v);
-                if (v) PL.set(np++, pj);
-            }
-            const float tx = rx, ty = ry;
-            if (lp2(PL, np, radius, -li.w, li.z, rx, ry, true) < np) { rx = tx; ry = ty; }
-            distance = det2(li.z, li.w, li.x - rx, li.y - ry);
-        }
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// register-resident RVO2 for simulators of <= 10 agents (<= 9 ORCA lines): every line index is a
-// compile-time constant after full unrolling, so lines / projected lines live in VGPRs
-// ------------------------------------------------------------------------------------------------
-#define RMM 9
-
-// linearProgram1, branch-free over the earlier lines: RVO2 exits as soon as tLeft > tRight or a
-// parallel line has numerator < 0; tLeft only grows and tRight only shrinks, so "exit at some prefix"
-// equals "tLeft > tRight at the end", and the parallel-line test is order independent. Evaluating all
-// lines first gives the same result while the divisions are independent (ILP).
-__device__ __forceinline__ bool lp1_core(const float4 ln, const float4 (&L)[RMM], const bool (&V)[RMM], const int no,
-                                         bool useV, float radius, float &tL, float &tR)
-{
-    const float dot = ln.x * ln.z + ln.y * ln.w;
-    const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
-    bool fail = disc < 0.0f;
-    const float sd = fsqrt(disc);
-    tL = -dot - sd;
-    tR = -dot + sd;
-#pragma unroll
-    for (int i = 0; i < RMM; ++i) {
-        if (i < no && (!useV || V[i])) {
-            const float4 li = L[i];
-            const float den = det2(ln.z, ln.w, li.z, li.w);
-            const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
-            const bool par = fabsf(den) <= RVO_EPSILON;
-            fail = fail || (par && num < 0.0f);
-            const float t = fdiv(num, den);
-            tR = (!par && den >= 0.0f && t < tR) ? t : tR;
-            tL = (!par && !(den >= 0.0f) && tL < t) ? t : tL;
-        }
-    }
-    return !(fail || tL > tR);
-}
-
-__device__ __forceinline__ bool lp1_r(const float4 (&L)[RMM], const int no, float radius, float ox, float oy,
-                                      bool dirOpt, float &rx, float &ry)
-{
-    const float4 ln = L[no];
-    float tL, tR;
-    const bool V[RMM] = {};
-    if (!lp1_core(ln, L, V, no, false, radius, tL, tR)) return false;
-    if (dirOpt) {
-        if (ox * ln.z + oy * ln.w > 0.0f) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
-        else { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
-    } else {
-        const float t = ln.z * (ox - ln.x) + ln.w * (oy - ln.y);
-        if (t < tL) { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
-        else if (t > tR) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
-        else { rx = ln.x + t * ln.z; ry = ln.y + t * ln.w; }
-    }
-    return true;
-}
-
-// linearProgram1 (direction-optimal) over projected lines with RVO2's skipped ones marked invalid
-__device__ __forceinline__ bool lp1p_r(const float4 (&P)[RMM], const bool (&V)[RMM], const int no, float radius,
-                                       float ox, float oy, float &rx, float &ry)
-{
-    const float4 ln = P[no];
-    float tL, tR;
-    if (!lp1_core(ln, P, V, no, true, radius, tL, tR)) return false;
-    if (ox * ln.z + oy * ln.w > 0.0f) { rx = ln.x + tR * ln.z; ry = ln.y + tR * ln.w; }
-    else { rx = ln.x + tL * ln.z; ry = ln.y + tL * ln.w; }
-    return true;
-}
-
-__device__ __forceinline__ int lp2_r(const float4 (&L)[RMM], int n, float radius, float ox, float oy, float &rx,
-                                     float &ry)
-{
-    if (ox * ox + oy * oy > radius * radius) {
-        const float inv = fdiv(1.0f, fsqrt(ox * ox + oy * oy));
-        rx = (ox * inv) * radius; ry = (oy * inv) * radius;
-    } else { rx = ox; ry = oy; }
-#pragma unroll
-    for (int i = 0; i < RMM; ++i) {
-        if (i < n) {
-            const float4 li = L[i];
-            if (det2(li.z, li.w, li.x - rx, li.y - ry) > 0.0f) {
-                const float tx = rx, ty = ry;
-                if (!lp1_r(L, i, radius, ox, oy, false, rx, ry)) { rx = tx; ry = ty; return i; }
-            }
-        }
-    }
-    return n;
-}
-
-__device__ __forceinline__ void lp3_r(const float4 (&L)[RMM], int n, int begin, float radius, float &rx, float &ry)
-{
-    float distance = 0.0f;
-#pragma unroll
-    for (int i = 0; i < RMM; ++i) {
-        if (i >= begin && i < n) {
-            const float4 li = L[i];
-            if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
-                float4 P[RMM];
-                bool V[RMM];
-#pragma unroll
-                for (int j = 0; j < RMM; ++j) {
-                    V[j] = false;
-                    P[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (j < i) P[j] = proj_line(li, L[j], V[j]);
-                }
-                const float tx = rx, ty = ry;
-                const float ox = -li.w, oy = li.z;   // linearProgram2(projLines, radius, (-d.y, d.x), true)
-                rx = ox * radius; ry = oy * radius;
-                bool fail = false;
-#pragma unroll
-                for (int k = 0; k < RMM; ++k) {
-                    if (k < i && V[k] && !fail) {
-                        const float4 pk = P[k];
-                        if (det2(pk.z, pk.w, pk.x - rx, pk.y - ry) > 0.0f) {
-                            const float sx = rx, sy = ry;
-                            if (!lp1p_r(P, V, k, radius, ox, oy, rx, ry)) { rx = sx; ry = sy; fail = true; }
-                        }
-                    }
-                }
-                if (fail) { rx = tx; ry = ty; }
-                distance = det2(li.z, li.w, li.x - rx, li.y - ry);
-            }
-        }
-    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -800,6 +613,49 @@ __device__ __forceinline__ float4 orca_line(float X0, float Y0, float VX0, float
         ux = s * uwx; uy = s * uwy;
     }
     return make_float4(VX0 + 0.5f * ux, VY0 + 0.5f * uy, dx, dy);
+}
+
+// Agent::computeNeighbors + the agent loop of Agent::computeNewVelocity for a simulator of <= 10 agents
+// (RVO2's KdTree is a single leaf: the neighbours are the in-range slots stably sorted by distSq in slot
+// order), quad-cooperative: lane sq builds the lines of slots sq, sq+4, sq+8 and ranks them itself.
+// `slot(k, x, y, vx, vy, r)` gives observed slot k (agent k + 1) in float32. Lines land in Lb[rank];
+// D is [M] distSq scratch. Returns the number of lines. Shared by cn_step_kernel and cn_debug_orca.
+template <typename SlotF>
+__device__ __forceinline__ int orca_lines_quad(const SlotF &slot, int M, int sq, float X0, float Y0, float VX0,
+                                               float VY0, float R0, float rangeSq, float invTH, float invTS,
+                                               float4 *Lb, float *D)
+{
+    float4 rawv[3];
+    float dv[3];
+    uint32_t inm = 0;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+        const int k = sq + 4 * u;
+        rawv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        dv[u] = 0.0f;
+        if (k < M) {
+            float x, y, vx, vy, r;
+            slot(k, x, y, vx, vy, r);
+            const float dx = X0 - x, dy = Y0 - y;
+            dv[u] = dx * dx + dy * dy;
+            if (dv[u] < rangeSq) inm |= 1u << k;
+            rawv[u] = orca_line(X0, Y0, VX0, VY0, R0, x, y, vx, vy, r, invTH, invTS);
+            D[k] = dv[u];
+        }
+    }
+    inm = (uint32_t)quad_or((int)inm);
+    wsync();
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+        const int k = sq + 4 * u;
+        if (k < M && ((inm >> k) & 1u)) {
+            int rank = 0;
+            for (int q = 0; q < M; ++q)
+                if (((inm >> q) & 1u) && (D[q] < dv[u] || (D[q] == dv[u] && q < k))) ++rank;
+            Lb[rank] = rawv[u];
+        }
+    }
+    return __popc(inm);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1865,39 +1721,12 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 int cnt = 0;
                 uint32_t inm = 0;
                 if constexpr (!KD) {
-                  if (hq) {
-                    float *D = sl.nd + h * M;
-                    float4 rawv[3];
-                    float dv[3];
-#pragma unroll
-                    for (int u = 0; u < 3; ++u) {
-                        const int k = sq + 4 * u;
-                        rawv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                        dv[u] = 0.0f;
-                        if (k < M) {
-                            float x, y, vx, vy, r;
+                  if (hq)
+                    cnt = orca_lines_quad(
+                        [&](int k, float &x, float &y, float &vx, float &vy, float &r) {
                             slot_agent(sl, c, eb, elq, EPB, N, iq, k, visq, dmq, rdummy, x, y, vx, vy, r);
-                            const float dx = X0 - x, dy = Y0 - y;
-                            dv[u] = dx * dx + dy * dy;
-                            if (dv[u] < rangeSq) inm |= 1u << k;
-                            rawv[u] = orca_line(X0, Y0, VX0, VY0, R0, x, y, vx, vy, r, invTH, invTS);
-                            D[k] = dv[u];
-                        }
-                    }
-                    inm = (uint32_t)quad_or((int)inm);
-                    wsync();
-#pragma unroll
-                    for (int u = 0; u < 3; ++u) {
-                        const int k = sq + 4 * u;
-                        if (k < M && ((inm >> k) & 1u)) {
-                            int rank = 0;
-                            for (int q = 0; q < M; ++q)
-                                if (((inm >> q) & 1u) && (D[q] < dv[u] || (D[q] == dv[u] && q < k))) ++rank;
-                            Lb[rank] = rawv[u];
-                        }
-                    }
-                    cnt = __popc(inm);
-                  }
+                        },
+                        M, sq, X0, Y0, VX0, VY0, R0, rangeSq, invTH, invTS, Lb, sl.nd + h * M);
                 } else {
                     // (1) the quad loads the persisted KdTree order and fills, in that order, the agents'
                     //     positions (XYP[q] = agent perm[q]: self = 0, slot k = k + 1; kept in the projected-
@@ -2197,13 +2026,9 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             else if (cd < dmin) dmin = cd;
             if (c.norm_zones && !nz_checked) {
                 nz_checked = true;
-                double zx[4], zy[4];
-                for (int z = 0; z < 2 && !nz_viol; ++z) {
-                    norm_zone(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB),
-                              RF(sl, R_VY, re, EPB), rr, (flags & CN_FLAG_ROBOT_F32) != 0, c.norm_zone_lhs, z == 0, zx,
-                              zy);
-                    if (disc_quad_intersect(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), rr, zx, zy)) nz_viol = true;
-                }
+                nz_viol = robot_norm_zone_violation(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB),
+                                                    RF(sl, R_VY, re, EPB), rr, (flags & CN_FLAG_ROBOT_F32) != 0,
+                                                    c.norm_zone_lhs);
             }
             const uint32_t f = sl.lf[eb + k];
             vr_viol += (f & LF_VR) ? 1 : 0;
@@ -2655,6 +2480,38 @@ __global__ void __launch_bounds__(64) cn_disc_quad_kernel(int64_t n, int mode, c
                   : disc_quad_intersect(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i);
 }
 
+// cn_debug_orca: one quad per simulator (16 per 64-lane workgroup), the step kernel's quad-path functions
+__global__ void __launch_bounds__(64) cn_orca_kernel(int64_t n, int A, const float *__restrict__ ag,
+                                                     const float *__restrict__ self, float nd, float th, float ts,
+                                                     float *__restrict__ out)
+{
+    __shared__ float4 Ls[16][9], Ps[16][9];
+    __shared__ float Ds[16][9];
+    const int q = threadIdx.x >> 2, sq = threadIdx.x & 3;
+    const int64_t i = (int64_t)blockIdx.x * 16 + q;
+    const bool act = i < n;
+    const float *a = ag + (act ? i : 0) * A * 5;
+    const int M = A - 1;
+    int cnt = 0;
+    if (act)
+        cnt = orca_lines_quad(
+            [&](int k, float &x, float &y, float &vx, float &vy, float &r) {
+                const float *o = a + (k + 1) * 5;
+                x = o[0]; y = o[1]; vx = o[2]; vy = o[3]; r = o[4];
+            },
+            M, sq, a[0], a[1], a[2], a[3], a[4], nd * nd, fdiv(1.0f, th), fdiv(1.0f, ts), Ls[q], Ds[q]);
+    wsync();
+    if (act) {
+        const float vmax = self[3 * i], ox = self[3 * i + 1], oy = self[3 * i + 2];
+        float rx, ry;
+        const int fail_at = lp2_q(Ls[q], cnt, vmax, ox, oy, sq, rx, ry);
+        if (fail_at < cnt) lp3_q(Ls[q], Ps[q], cnt, fail_at, vmax, sq, rx, ry);
+        if (sq == 0) {
+            out[4 * i] = rx; out[4 * i + 1] = ry; out[4 * i + 2] = (float)fail_at; out[4 * i + 3] = (float)cnt;
+        }
+    }
+}
+
 extern "C" {
 
 const char *cn_last_error(void) { return g_err; }
@@ -2977,6 +2834,17 @@ int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, cons
     if (n <= 0 || !px || !py || !r || !qx || !qy || !out) return set_err(CN_EINVAL, "cn_debug_disc_quad: n > 0 and buffers required");
     hipLaunchKernelGGL(cn_disc_quad_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, n, mode,
                        px, py, r, qx, qy, out);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
+
+int cn_debug_orca(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
+                  float time_horizon, float time_step, float *out)
+{
+    if (n <= 0 || !agents || !self || !out) return set_err(CN_EINVAL, "cn_debug_orca: n > 0 and buffers required");
+    if (A < 1 || A > 10) return set_err(CN_EUNSUPPORTED, "cn_debug_orca: 1 <= A <= 10 (the quad path)");
+    hipLaunchKernelGGL(cn_orca_kernel, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, (hipStream_t)stream, n, A,
+                       agents, self, neighbor_dist, time_horizon, time_step, out);
     HIPCHK(hipGetLastError());
     return CN_OK;
 }

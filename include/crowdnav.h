@@ -234,6 +234,16 @@ int cn_lidar_obs(cn_engine *eng, void *stream, const uint8_t *reset_mask, int en
 int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, const double *py, const double *r,
                        const double *qx, const double *qy, int32_t *out);
 
+/* Test hook (SURVEY Appendix A.4 known answers): agent 0's new velocity of n independent RVO2 simulators
+ * of A <= 10 agents each (crowd_nav/policy/orca.py:92-136: addAgent / setAgentPrefVelocity / doStep /
+ * getAgentVelocity(0)), through the step kernel's own code path (quad-cooperative neighbour ranking and
+ * ORCA lines, linearProgram2, linearProgram3). agents [n][A][5] = (px, py, vx, vy, radius) with agent 0 =
+ * self; self [n][3] = (maxSpeed, prefVelocity.x, prefVelocity.y); neighbor_dist, time_horizon, time_step
+ * as in PyRVOSimulator. out [n][4] = (vx, vy, index of the line linearProgram2 failed at or the line
+ * count when it succeeded, the line count). Checked against oracle/cpu_ref.c:cnref_rvo2_agent0 and hand-derived answers. */
+int cn_debug_orca(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
+                  float time_horizon, float time_step, float *out);
+
 /* out[r][h] = sum_n hs[r][n][h] * attn[r][n]; hs [R][N][H], attn [R][N], out [R][H]; H % 4 == 0. */
 int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, float *out);
 

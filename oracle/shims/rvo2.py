@@ -6,7 +6,8 @@ code (x86-64 SSE, no FMA contraction). Only agent 0's new velocity is computed i
 reads only getAgentVelocity(0) and overwrites every agent's position and velocity before the next
 doStep (orca.py:110-136), so the other agents' updates are unobservable. The KdTree's agent order
 (KdTree::agents_) persists across doStep calls exactly as in RVO2.
-PARITY UNPINNED (no RVO2 binary exists here); pinned only by analytic known answers.
+PARITY vs the real RVO2 UNPINNED (no RVO2 binary exists here); pinned by the analytic known answers of
+SURVEY Appendix A.4 in tests/test_orca_known_answers.py (which also checks it equals oracle/cpu_ref.c).
 """
 import numpy as np
 
