@@ -118,15 +118,39 @@ def cpu_baseline(N, budget_s=12.0):
                       "%d envs x %d steps of the same C2 workload (%.1f s)" % (E, steps, el)}
 
 
-def load_pmc_traffic():
-    """HBM bytes per step-kernel launch from the committed rocprofv3 --pmc summary (profiles/), or None."""
-    p = os.path.join(REPO, "profiles", "pmc_step_kernel.json")
-    if not os.path.exists(p):
+def load_pmc(kernel="cn_step_kernel", workload="c2"):
+    """Counter figures for `kernel` from the newest committed rocprofv3 summary (profiles/pmc_<tag>.json,
+    written by profiles/summarize.py) that was measured on a library built from EXACTLY the sources this
+    run uses (CN_SRC_HASH) and on the same workload; None when no such profile exists (a stale profile
+    is never reported)."""
+    import glob
+
+    from crowdnav_dsrnn_amd import build
+
+    want = build.source_hash()
+    best = None
+    for p in glob.glob(os.path.join(REPO, "profiles", "pmc_*.json")):
+        try:
+            doc = json.load(open(p))
+        except Exception:
+            continue
+        if doc.get("lib_src_hash") != want:
+            continue
+        wl = "c2"
+        a = doc.get("bench_args", "").split()
+        if "--workload" in a:
+            wl = a[a.index("--workload") + 1]
+        if wl != workload:
+            continue
+        for k, d in doc.get("kernels", {}).items():
+            if kernel in k and "hbm_bytes_per_launch" in d:
+                if best is None or os.path.getmtime(p) > best[0]:
+                    best = (os.path.getmtime(p), doc["tag"], d)
+    if best is None:
         return None
-    try:
-        return float(json.load(open(p))["hbm_bytes_per_launch"])
-    except Exception:
-        return None
+    _, tag, d = best
+    return {"tag": tag, "traffic": d["hbm_bytes_per_launch"], "valu_issue_frac": d.get("valu_issue_frac"),
+            "active_inst_frac": d.get("active_inst_frac"), "avg_duration_ns": d.get("avg_duration_ns")}
 
 
 def run_c4(args, torch, dist, device, rank, world):
@@ -294,7 +318,7 @@ def main():
         kernel_s = a_ms.value / 1e3 / max(n.value, 1)
         bpl = algorithmic_bytes_per_env_step(eng.N) * eng.E   # the timed kernel is engs[0]'s
         achieved = bpl / kernel_s / 1e9
-        traffic = load_pmc_traffic() if args.workload == "c2" else None
+        pmc = load_pmc("cn_step_kernel", args.workload)
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -322,9 +346,13 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": traffic,
+                "traffic": round(pmc["traffic"]) if pmc else None,
                 "kernel": "cn_step_kernel",
                 "algorithmic_bytes_per_launch": bpl,
+                # what actually limits the kernel: dependent per-lane chains, not bandwidth
+                "limiter": "latency / issue (dependent f64 + f32 chains per lane; not HBM)",
+                "valu_issue_frac": round(pmc["valu_issue_frac"], 4) if pmc and pmc["valu_issue_frac"] else None,
+                "pmc_profile": ("profiles/pmc_%s.json" % pmc["tag"]) if pmc else None,
             },
         }
         if not args.no_cpu_baseline and world == 1 and args.workload == "c2":

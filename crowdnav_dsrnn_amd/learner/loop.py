@@ -12,6 +12,7 @@ import time
 
 import torch
 
+from ..policy.utils import update_linear_schedule
 from .storage import RolloutStorage, SRNNRolloutStorage
 
 
@@ -42,6 +43,10 @@ class RolloutTrainer:
         self.srnn = getattr(actor_critic, "srnn", False) and isinstance(self.rollouts, SRNNRolloutStorage)
         self.episode_returns = []
         self.env_steps = 0
+        # train.py:203-207: num_updates over the global env count (sharded runs: nenv of the engine)
+        nenv = getattr(envs.engine.cfg, "nenv", envs.num_envs) or envs.num_envs
+        self.num_updates = max(int(config.training.num_env_steps) // config.ppo.num_steps // nenv, 1)
+        self.update_index = 0
 
     @torch.no_grad()
     def collect(self):
@@ -65,6 +70,10 @@ class RolloutTrainer:
 
     def update(self):
         t0 = time.perf_counter()
+        c = self.config
+        if c.training.use_linear_lr_decay:   # train.py:216-222, before the rollout of update j
+            update_linear_schedule(self.agent.optimizer, self.update_index, self.num_updates, c.training.lr)
+        self.update_index += 1
         ep_sum, ep_cnt = self.collect()
         r = self.rollouts
         with torch.no_grad():
@@ -72,7 +81,6 @@ class RolloutTrainer:
             next_value = self.ac.get_value(last,
                                            r.hidden(r.num_steps),
                                            r.masks[-1]).detach()
-        c = self.config
         r.compute_returns(next_value, c.ppo.use_gae, c.reward.gamma, c.ppo.gae_lambda,
                           c.training.use_proper_time_limits)
         t1 = time.perf_counter()

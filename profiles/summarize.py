@@ -1,13 +1,19 @@
-"""Summarise rocprofv3 CSV output into committed profile files.
+"""Summarise a rocprofv3 collection (profiles/run_profile.sh) into committed profile files.
 
-    python profiles/summarize.py <rocprof out dir> <tag>
+    python profiles/summarize.py gpurun_out/prof_<tag> <tag>
 
-Writes profiles/<tag>_kernel_stats.csv (copy of the kernel stats), profiles/<tag>_summary.txt and
-profiles/pmc_step_kernel.json (HBM bytes per cn_step_kernel launch, read by bench.py as
-roofline.traffic). HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB;
-on gfx950 FETCH_SIZE reads 1/2 of the bytes of wide coalesced streaming reads, so the read side is
-doubled (that correction is calibrated for 16-B-per-lane streaming loads; this kernel mixes 8-B
-loads, so the absolute figure carries that caveat — ratios are unaffected).
+Writes profiles/<tag>_kernel_stats.csv (the kernel-trace stats), profiles/<tag>_summary.txt and
+profiles/pmc_<tag>.json (per kernel: average duration, counters per launch, derived figures). The JSON
+records the library's CN_SRC_HASH (cn_version() on the box): bench.py takes `roofline.traffic` from
+the newest pmc_*.json whose hash equals the hash of the sources it runs, and reports null otherwise.
+
+HBM bytes follow MI355X_MICROARCH.md § HBM: FETCH_SIZE / WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
+reports 1/2 of the bytes of wide coalesced streaming reads, so the read side is doubled (calibrated for
+16-B-per-lane streaming loads; this kernel's loads are 8 B per lane, so the absolute read figure carries
+that caveat). Infinity-Cache hits are counted as fabric traffic by these counters.
+VALU-issue fraction = SQ_INSTS_VALU x 2 cycles (one wave64 VALU instruction occupies a SIMD's issue for
+2 cycles; f64 FMA/MUL/ADD take 4, transcendentals 8 on f64 per the microarchitecture guide's
+issue-cost table) / (1024 SIMDs x kernel cycles at 2.4 GHz).
 """
 import csv
 import glob
@@ -16,60 +22,86 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+CLOCK_HZ = 2.4e9
+SIMDS = 1024
 
 
 def find(d, pat):
-    f = glob.glob(os.path.join(d, "**", pat), recursive=True)
+    f = sorted(glob.glob(os.path.join(d, "**", pat), recursive=True))
     return f[0] if f else None
 
 
-def per_kernel_counter(path, counter):
-    vals = {}
+def counters(path):
+    """{kernel: {counter: [per-dispatch values]}} from a counter_collection.csv"""
+    out = {}
     if not path:
-        return vals
+        return out
     for row in csv.DictReader(open(path)):
-        if row.get("Counter_Name") != counter:
-            continue
         k = row.get("Kernel_Name", "")
-        vals.setdefault(k, []).append(float(row["Counter_Value"]))
-    return vals
+        out.setdefault(k, {}).setdefault(row["Counter_Name"], {})
+        d = out[k][row["Counter_Name"]]
+        disp = row.get("Dispatch_Id", str(len(d)))
+        d[disp] = d.get(disp, 0.0) + float(row["Counter_Value"])
+    return {k: {c: list(v.values()) for c, v in cs.items()} for k, cs in out.items()}
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")[:48]
 
 
 def main():
     out, tag = sys.argv[1], sys.argv[2]
+    ver = open(os.path.join(out, "lib_version.txt")).read().strip() if os.path.exists(
+        os.path.join(out, "lib_version.txt")) else ""
+    src_hash = ver.split("CN_SRC_HASH=", 1)[1][:64] if "CN_SRC_HASH=" in ver else None
+    args = open(os.path.join(out, "bench_args.txt")).read().strip() if os.path.exists(
+        os.path.join(out, "bench_args.txt")) else ""
     stats = find(os.path.join(out, "kt"), "*kernel_stats.csv")
-    lines = ["rocprofv3 --kernel-trace --stats  (bench.py --steps 400 --warmup 40, 4096 envs x 10 humans, C2)", ""]
-    avg = {}
+    lines = ["rocprofv3 collection %s: bench.py %s" % (tag, args), "library: %s" % ver, ""]
+    res = {}
     if stats:
         rows = list(csv.DictReader(open(stats)))
         with open(os.path.join(HERE, "%s_kernel_stats.csv" % tag), "w") as f:
             w = csv.DictWriter(f, fieldnames=rows[0].keys())
             w.writeheader()
             w.writerows(rows)
+        lines.append("--kernel-trace --stats")
         for r in rows:
-            name = r["Name"]
-            avg[name] = float(r["AverageNs"])
-            lines.append("%-40s calls=%-6s avg=%10.1f ns  min=%10.1f  max=%10.1f  total%%=%s" % (
-                name[:40], r["Calls"], float(r["AverageNs"]), float(r["MinNs"]), float(r["MaxNs"]),
+            res.setdefault(r["Name"], {})["avg_duration_ns"] = float(r["AverageNs"])
+            res[r["Name"]]["calls"] = int(r["Calls"])
+            lines.append("  %-48s calls=%-6s avg=%10.1f ns  min=%10.1f  max=%10.1f  total%%=%s" % (
+                short(r["Name"]), r["Calls"], float(r["AverageNs"]), float(r["MinNs"]), float(r["MaxNs"]),
                 r.get("Percentage", "")))
-    fetch = per_kernel_counter(find(os.path.join(out, "fetch"), "*counter_collection.csv"), "FETCH_SIZE")
-    write = per_kernel_counter(find(os.path.join(out, "write"), "*counter_collection.csv"), "WRITE_SIZE")
+    merged = {}
+    for p in ("fetch", "write", "sq1", "sq2", "tcc"):
+        for k, cs in counters(find(os.path.join(out, p), "*counter_collection.csv")).items():
+            for c, v in cs.items():
+                merged.setdefault(k, {})[c] = sum(v) / len(v)
     lines.append("")
-    pmc = {}
-    for k in sorted(set(fetch) | set(write)):
-        f = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [1])), 1)
-        w = sum(write.get(k, [0])) / max(len(write.get(k, [1])), 1)
-        hbm = (2.0 * f + w) * 1024.0
-        pmc[k] = {"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": hbm}
-        lines.append("%-40s FETCH_SIZE=%10.1f KiB  WRITE_SIZE=%10.1f KiB  HBM(2*fetch+write)=%12.0f B/launch" % (
-            k[:40], f, w, hbm))
-    step = [k for k in pmc if "cn_step_kernel" in k]
-    if step:
-        d = dict(pmc[step[0]])
-        d["kernel"] = step[0]
-        d["avg_duration_ns"] = next((v for n, v in avg.items() if "cn_step_kernel" in n), None)
-        d["source"] = "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (%s)" % tag
-        json.dump(d, open(os.path.join(HERE, "pmc_step_kernel.json"), "w"), indent=1)
+    lines.append("counters per launch (mean over dispatches)")
+    for k in sorted(merged):
+        d = res.setdefault(k, {})
+        d["counters"] = merged[k]
+        c = merged[k]
+        lines.append("  %s" % short(k))
+        for n in sorted(c):
+            lines.append("    %-28s %.6g" % (n, c[n]))
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            d["hbm_bytes_per_launch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+            lines.append("    => HBM bytes/launch (2*FETCH_SIZE + WRITE_SIZE) = %.0f" % d["hbm_bytes_per_launch"])
+        dur = d.get("avg_duration_ns")
+        if dur and "SQ_INSTS_VALU" in c:
+            cyc = dur * 1e-9 * CLOCK_HZ
+            d["valu_issue_frac"] = c["SQ_INSTS_VALU"] * 2.0 / (SIMDS * cyc)
+            lines.append("    => VALU-issue fraction (INSTS_VALU x 2 cyc / (1024 SIMD x %.0f cyc)) = %.4f" % (
+                cyc, d["valu_issue_frac"]))
+        if "SQ_WAVE_CYCLES" in c and "SQ_ACTIVE_INST_ANY" in c:
+            d["active_inst_frac"] = c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+            d["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
+            lines.append("    => per-wave: issuing %.3f, parked on waitcnt/barrier %.3f of wave cycles" % (
+                d["active_inst_frac"], d["wait_any_frac"]))
+    doc = {"tag": tag, "bench_args": args, "lib_version": ver, "lib_src_hash": src_hash, "kernels": res}
+    json.dump(doc, open(os.path.join(HERE, "pmc_%s.json" % tag), "w"), indent=1)
     open(os.path.join(HERE, "%s_summary.txt" % tag), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
