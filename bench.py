@@ -94,28 +94,68 @@ def engines_for(workload, E, N, rank, world, rng="mt19937"):
     return out
 
 
-def cpu_baseline(N, budget_s=12.0):
-    """The oracle (C restatement of the reference step, oracle/cpu_ref.c) on ONE host core, bounded
-    sample of the same workload: 256 envs, steps until ~budget_s of CPU time."""
+def _oracle_rate(cfg, budget_s, threads, kind="uniform"):
+    """env-steps/s of oracle/cpu_ref.c on `cfg` with `threads` OpenMP threads over envs, ~budget_s."""
     from oracle import cpu_ref
 
-    cpu_ref.lib().cnref_set_threads(1)
-    E = 256
-    cfg = make_config(E, N, 0, 4096)
+    cpu_ref.lib().cnref_set_threads(threads)
+    E = cfg.num_envs
     eng = cpu_ref.RefEngine(cfg)
     eng.reset()
     rng = np.random.RandomState(0)
     steps = 0
     t0 = time.perf_counter()
     while True:
-        eng.step(rng.uniform(-0.1, 0.1, (E, 2)).astype(np.float32))
+        a = rng.uniform(-0.1, 0.1, (E, 2)) if kind == "uniform" else rng.normal(0, 0.5, (E, 2))
+        eng.step(a.astype(np.float32))
         steps += 1
         el = time.perf_counter() - t0
         if el > budget_s or steps >= 50000:
             break
-    return {"value": E * steps / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": "oracle/cpu_ref.c (C restatement of CrowdSimDict.step incl. RVO2 ORCA), 1 thread, "
-                      "%d envs x %d steps of the same C2 workload (%.1f s)" % (E, steps, el)}
+    return E * steps / el, steps, el
+
+
+def host_threads():
+    """CPU threads this process may use: the box's share (OMP_NUM_THREADS = 16 there), else the affinity."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(env))) if env and env.isdigit() else n
+
+
+def cpu_baseline(N, budget_s=12.0):
+    """SURVEY §8d CPU legs on the GPU box's host, bounded samples of the same C2 workload:
+    value = oracle/cpu_ref.c (C restatement of CrowdSimDict.step incl. RVO2 ORCA) with an OpenMP loop
+    over envs on all the host threads this job may use; one_thread = the same on 1 thread; and the
+    reference's own Python step, estimated as cpu_ref(social force, 1 thread, timed here) / the
+    cpu_ref-over-reference ratio measured in the build container (profiles/cpu_reference_step.json,
+    oracle/time_reference_step.py: ORCA needs the absent RVO2, so the reference is timed with social force)."""
+    from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config
+
+    T = host_threads()
+    E_all = max(256, 64 * T)
+    all_rate, all_steps, all_el = _oracle_rate(make_config(E_all, N, 0, 4096), budget_s * 0.5, T)
+    one_rate, one_steps, one_el = _oracle_rate(make_config(256, N, 0, 4096), budget_s * 0.3, 1)
+    out = {"value": all_rate, "unit": "env-steps/s", "cores": T, "kind": "port",
+           "sample": "oracle/cpu_ref.c (C restatement of CrowdSimDict.step incl. RVO2 ORCA), OpenMP over envs on "
+                     "%d threads, %d envs x %d steps of the same C2 workload (%.1f s)" % (T, E_all, all_steps, all_el),
+           "one_thread": {"value": one_rate, "cores": 1,
+                          "sample": "same, 1 thread, 256 envs x %d steps (%.1f s)" % (one_steps, one_el)}}
+    cal = os.path.join(REPO, "profiles", "cpu_reference_step.json")
+    if os.path.exists(cal):
+        doc = json.load(open(cal))
+        c = clone_config(Config())
+        c.sim.human_num = 10
+        c.humans.policy = "social_force"
+        c.action_space.kinematics = "holonomic"
+        c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+        sf_rate, _, _ = _oracle_rate(make_cn_config(c, num_envs=256, nenv=256, phase="train"), budget_s * 0.2, 1,
+                                     kind="normal")
+        out["reference_python_estimate"] = {
+            "value": sf_rate / doc["ratio_oracle_over_reference"], "cores": 1,
+            "sample": "reference CrowdSimDict.step (social force, N=10, 1 env, 1 core): %.1f env-steps/s timed in the "
+                      "build container; scaled to this host by cpu_ref(social force) here / there (ratio %.1f)"
+                      % (doc["reference_env_steps_per_s"], doc["ratio_oracle_over_reference"])}
+    return out
 
 
 def load_pmc(kernel="cn_step_kernel", workload="c2"):

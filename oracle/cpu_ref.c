@@ -736,6 +736,45 @@ EXPORT void cnref_disc_quad(int64_t n, const double *px, const double *py, const
     for (int64_t i = 0; i < n; ++i) out[i] = disc_quad_intersect(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i);
 }
 
+/* test hook: how far the robot's norm-zone predicate is from its decision boundary. For each of the two
+ * zones (norm_zone, crowd_sim.py:918-926) the separating-axis gap between the robot's 64-gon and the zone
+ * over all 68 unit edge normals (> 0 separated by that distance, <= 0 overlapping: max over axes of the
+ * gap); returns the zone value closest to 0 in magnitude. A GPU/oracle disagreement on the penalty is
+ * legitimate only when this is within rounding of 0 (the zone corner touches the disc). */
+EXPORT double cnref_norm_zone_margin(double px, double py, double vx, double vy, double r, int f32, int lhs)
+{
+    double best = INFINITY;
+    for (int z = 0; z < 2; ++z) {
+        double qx[4], qy[4], vxs[64], vys[64];
+        norm_zone(px, py, vx, vy, r, f32, lhs, z == 0, qx, qy);
+        for (int k = 0; k < 64; ++k) {
+            const double ang = -(k * (M_PI / 2 / 16));
+            vxs[k] = px + r * cos(ang);
+            vys[k] = py + r * sin(ang);
+        }
+        vxs[0] = px + r; vys[0] = py;
+        double gap = -INFINITY;
+        for (int p = 0; p < 2; ++p) {
+            const int nv = p ? 64 : 4;
+            const double *ex_ = p ? vxs : qx, *ey_ = p ? vys : qy;
+            for (int k = 0; k < nv; ++k) {
+                const double ex = ex_[(k + 1) % nv] - ex_[k], ey = ey_[(k + 1) % nv] - ey_[k];
+                const double len = sqrt(ex * ex + ey * ey);
+                if (len == 0.0) continue;
+                const double nx = -ey / len, ny = ex / len;
+                double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+                for (int v = 0; v < 64; ++v) { const double t = vxs[v] * nx + vys[v] * ny; amin = t < amin ? t : amin; amax = t > amax ? t : amax; }
+                for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
+                const double g1 = bmin - amax, g2 = amin - bmax;
+                const double gg = g1 > g2 ? g1 : g2;
+                gap = gg > gap ? gg : gap;
+            }
+        }
+        if (fabs(gap) < fabs(best)) best = gap;
+    }
+    return best;
+}
+
 /* ------------------------------------------------------------------------------------------------ */
 /* spawn (crowd_sim.py:296-393, 555-663)                                                             */
 /* ------------------------------------------------------------------------------------------------ */

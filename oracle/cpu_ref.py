@@ -41,6 +41,8 @@ def lib():
         L.cnref_rvo2_agent0.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
                                         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp]
         L.cnref_set_threads.argtypes = [ctypes.c_int]
+        L.cnref_norm_zone_margin.restype = ctypes.c_double
+        L.cnref_norm_zone_margin.argtypes = [ctypes.c_double] * 5 + [ctypes.c_int, ctypes.c_int]
         L.cnref_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -118,6 +120,12 @@ def philox4x32_10(ctr, key):
     out = np.zeros(4, np.uint32)
     lib().cnref_philox4x32_10(_p(c), _p(k), _p(out))
     return out
+
+
+def norm_zone_margin(px, py, vx, vy, r, f32, lhs):
+    """Signed distance of the robot's norm-zone predicate from its decision boundary (cpu_ref.c)."""
+    return lib().cnref_norm_zone_margin(float(px), float(py), float(vx), float(vy), float(r), int(bool(f32)),
+                                        int(lhs))
 
 
 def rvo2_agent0(X, Y, VX, VY, R, vmax, pref, neighbor_dist=10.0, time_horizon=5.0, time_step=0.25, perm=None):
