@@ -19,6 +19,8 @@ oracle/shims (gym, shapely, rvo2, torchvision — see oracle/shims/README.md) an
   convgru.npz    ConvGRU Policy.act / evaluate_actions with procedural weights (convgru_model.py, model.py)
   ppo.npz        SRNNRolloutStorage + compute_returns + PPO.update on procedural weights
                  (pytorchBaselines/a2c_ppo_acktr/storage.py:14-292, algo/ppo.py:36-118)
+  train_loop.npz train.py:219-330 for one update on real reference envs (act, step with auto-reset,
+                 insert, get_value, compute_returns, PPO.update; deterministic actions)
 
 The fixtures are data only (inputs and expected outputs); nothing of the reference's source is
 copied. The reference never travels to the GPU box; these .npz files do.
@@ -533,6 +535,92 @@ def gen_ppo(outdir):
     print("ppo ok")
 
 
+def gen_train_loop(outdir, N=5, E=4, T=32, epochs=2):
+    """The body of the reference's train.py:219-330 for one update, on real reference envs
+    (CrowdSimDict + the VecEnv worker's auto-reset, ORCA humans through the rvo2 stand-in) and the
+    reference Policy / SRNNRolloutStorage / PPO on procedural weights: act -> envs.step -> masks ->
+    rollouts.insert for num_steps steps, get_value, compute_returns (GAE, proper time limits), one
+    PPO.update (num_mini_batch 1: the minibatch permutation then only reorders a mean), after_update.
+    Actions are the policy's mode (deterministic=True): train.py samples them from the torch RNG, whose
+    stream a device-side sampler cannot reproduce; everything downstream of the action is unchanged."""
+    import torch
+
+    torch.set_num_threads(4)
+    import gym
+    from pytorchBaselines.a2c_ppo_acktr import algo
+    from pytorchBaselines.a2c_ppo_acktr.model import Policy
+    from pytorchBaselines.a2c_ppo_acktr.storage import SRNNRolloutStorage
+
+    cfg = make_ref_config(N=N)
+    cfg.training.cuda = False
+    cfg.training.num_processes = E
+    cfg.ppo.num_steps = T
+    cfg.ppo.num_mini_batch = 1
+    cfg.ppo.epoch = epochs
+    obs_space = {"robot_node": gym.spaces.Box(-np.inf, np.inf, (1, 7)),
+                 "temporal_edges": gym.spaces.Box(-np.inf, np.inf, (1, 2)),
+                 "spatial_edges": gym.spaces.Box(-np.inf, np.inf, (N, 2))}
+    act_space = gym.spaces.Box(-np.inf, np.inf, (2,))
+    torch.manual_seed(0)
+    pol = Policy(obs_space, act_space, base="srnn", base_kwargs=cfg)
+    pol.load_state_dict(procedural_state_dict(pol))
+    envs = [make_ref_env(cfg, r, E) for r in range(E)]
+    rol = SRNNRolloutStorage(T, E, obs_space, act_space, 128, 256, recurrent_cell_type="GRU")
+    obs = [obs32(env_reset(env)) for env in envs]
+    rol.obs["robot_node"][0].copy_(torch.from_numpy(np.stack([o[0] for o in obs])))
+    rol.obs["temporal_edges"][0].copy_(torch.from_numpy(np.stack([o[1] for o in obs])))
+    rol.obs["spatial_edges"][0].copy_(torch.from_numpy(np.stack([o[2] for o in obs])))
+    out = {"meta_" + k: np.array(v) for k, v in cfg_meta(cfg, E).items()}
+    out["T"], out["epochs"] = np.array(T), np.array(epochs)
+    rec = {k: [] for k in ("action", "value", "logp", "reward", "done", "robot_node", "spatial")}
+    for step in range(T):
+        with torch.no_grad():
+            o_s = {k: rol.obs[k][step] for k in rol.obs}
+            h_s = {k: rol.recurrent_hidden_states[k][step] for k in rol.recurrent_hidden_states}
+            value, action, logp, hxs = pol.act(o_s, h_s, rol.masks[step], deterministic=True)
+        res = [env_step(env, action[e].numpy().copy()) for e, env in enumerate(envs)]
+        ob = [obs32(r[0]) for r in res]
+        t_obs = {"robot_node": torch.from_numpy(np.stack([o[0] for o in ob])),
+                 "temporal_edges": torch.from_numpy(np.stack([o[1] for o in ob])),
+                 "spatial_edges": torch.from_numpy(np.stack([o[2] for o in ob]))}
+        reward = torch.tensor([[np.float32(r[1])] for r in res], dtype=torch.float32)
+        done = [r[2] for r in res]
+        masks = torch.FloatTensor([[0.0] if d else [1.0] for d in done])          # train.py:259-260
+        bad_masks = torch.FloatTensor([[1.0] for _ in done])                     # no 'bad_transition'
+        rol.insert(t_obs, hxs, action, logp, value, reward, masks, bad_masks)
+        rec["action"].append(action.numpy().copy())
+        rec["value"].append(value.numpy().copy())
+        rec["logp"].append(logp.numpy().copy())
+        rec["reward"].append(reward.numpy().copy())
+        rec["done"].append(np.array(done, np.uint8))
+        rec["robot_node"].append(t_obs["robot_node"].numpy().copy())
+        rec["spatial"].append(t_obs["spatial_edges"].numpy().copy())
+    with torch.no_grad():
+        next_value = pol.get_value({k: rol.obs[k][-1] for k in rol.obs},
+                                   {k: rol.recurrent_hidden_states[k][-1] for k in rol.recurrent_hidden_states},
+                                   rol.masks[-1]).detach()
+    rol.compute_returns(next_value, cfg.ppo.use_gae, cfg.reward.gamma, cfg.ppo.gae_lambda,
+                        cfg.training.use_proper_time_limits)
+    out["returns"] = rol.returns.numpy().copy()
+    agent = algo.PPO(pol, cfg.ppo.clip_param, epochs, 1, cfg.ppo.value_loss_coef, cfg.ppo.entropy_coef,
+                     lr=cfg.training.lr, eps=cfg.training.eps, max_grad_norm=cfg.training.max_grad_norm)
+    torch.manual_seed(99)
+    vl, al, de = agent.update(rol)
+    rol.after_update()
+    out["update_losses"] = np.array([vl, al, de])
+    for k, v in rec.items():
+        out[k] = np.stack(v)
+    for k, v in pol.state_dict().items():
+        out["param_" + k] = v.numpy().copy()
+    for k, v in rol.recurrent_hidden_states.items():
+        out["hxs0_after_" + k] = v[0].numpy().copy()
+    out["hparams"] = np.array([cfg.ppo.clip_param, cfg.ppo.value_loss_coef, cfg.ppo.entropy_coef, cfg.training.lr,
+                               cfg.training.eps, cfg.training.max_grad_norm, cfg.reward.gamma, cfg.ppo.gae_lambda,
+                               float(cfg.ppo.use_gae), float(cfg.training.use_proper_time_limits)])
+    np.savez_compressed(os.path.join(outdir, "train_loop.npz"), **out)
+    print("train_loop ok: dones", int(out["done"].sum()), "losses", out["update_losses"])
+
+
 def gen_lidar(name, cfg, E, resets, outdir):
     """Post-reset states + ConvGRU observations of the reference (LiDAR scan at reset)."""
     if not hasattr(np, "int"):
@@ -872,6 +960,8 @@ def main():
         gen_dsrnn(args.out)
     if want("ppo"):
         gen_ppo(args.out)
+    if want("train_loop"):
+        gen_train_loop(args.out)
     if want("eval"):
         gen_eval(args.out)
     def _radius(c, r):

@@ -1,3 +1,5 @@
+import builtins
+
 import numpy as np
 
 
@@ -13,4 +15,4 @@ class Box(object):
 
 class Dict(object):
     def __init__(self, spaces):
-        self.spaces = dict(spaces)
+        self.spaces = builtins.dict(spaces)   # a `gym.spaces.dict` submodule import shadows `dict` here

@@ -76,7 +76,7 @@ def _replay(z, E, env_offset=0, nenv=None, device="cpu"):
         te = torch.zeros(E, 1, 2)
         for i in range(E):
             rn[i, 0, :2] = torch.from_numpy(eps[g[i] % T]["first"])
-        return {"robot_node": rn, "temporal_edges": te}
+        return {"robot_node": rn.to(device), "temporal_edges": te.to(device)}
 
     rec.start(first_obs())
     for _ in range(100000):
@@ -227,3 +227,16 @@ def test_batched_evaluation_on_engine_matches_sequential():
         for a, b in zip(oE, o1):
             assert a == b
     assert sum(s1["num_events"][k]["total"] for k in s1["num_events"]) == 12
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["eval_social", "eval_sidepref"])
+@pytest.mark.parametrize("E", [1, 7, 40])
+def test_device_evaluation_matches_reference_log(case, E):
+    """EpisodeRecorder with its running sums on the GPU (the evaluate() path on a cuda VecEnv): the
+    reference's evaluate() log and returned lists (tests/golden/eval_*.npz, evaluation.py:96-330,
+    metrics.py:5-44) reproduced from device-side records, batched over E envs."""
+    z = load(case + ".npz")
+    rec, c = _replay(z, E, device="cuda:0")
+    assert all(v.device.type == "cuda" for v in rec.rec.values())
+    _check_against_golden(z, rec, c)

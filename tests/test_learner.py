@@ -216,3 +216,59 @@ def test_rollout_storage_vs_reference():
         st.after_update()
         np.testing.assert_array_equal(st.obs[0].numpy(), z["after_obs0"])
         np.testing.assert_array_equal(st.recurrent_hidden_states[0].numpy(), z["after_hxs0"])
+
+
+@pytest.mark.gpu
+def test_rollout_trainer_matches_reference_train_loop():
+    """RolloutTrainer (act -> step_device -> insert, masks from done on device, get_value,
+    compute_returns, PPO.update, after_update) with base='srnn' against the reference's train.py:219-330
+    loop body on real reference envs (tests/golden/train_loop.npz, oracle/gen_golden.py gen_train_loop):
+    4 envs x 5 humans, ORCA, holonomic, 32 steps with two episode ends, procedural weights, policy-mode
+    actions. Tolerances: actions / values 5e-5 (fp32 GEMM order, GPU vs CPU), rewards / returns 2e-4 (the
+    env consumes the slightly different actions), losses 1e-3 relative, parameters 2e-5 absolute."""
+    from crowdnav_dsrnn_amd.config import Config, clone_config
+    from crowdnav_dsrnn_amd.envs import CrowdNavVecEnv
+    from crowdnav_dsrnn_amd.learner.loop import RolloutTrainer
+
+    z = load("train_loop.npz")
+    Tn, En, ep = int(z["T"]), int(z["meta_E"]), int(z["epochs"])
+    Nn = int(z["meta_N"])
+    dev = "cuda:0"
+    c = clone_config(Config())
+    c.sim.human_num = Nn
+    c.humans.policy = "orca"
+    c.action_space.kinematics = "holonomic"
+    c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+    c.training.num_processes = En
+    c.ppo.num_steps = Tn
+    c.ppo.num_mini_batch = 1
+    c.ppo.epoch = ep
+    hp = z["hparams"]
+    assert (c.ppo.clip_param, c.ppo.value_loss_coef, c.ppo.entropy_coef, c.training.lr, c.training.eps,
+            c.training.max_grad_norm, c.reward.gamma, c.ppo.gae_lambda) == tuple(float(x) for x in hp[:8])
+    envs = CrowdNavVecEnv(c, En, c.env.seed, dev, nenv=En, phase="train")
+    pol = make_policy(Nn, E=En, T=Tn, device=dev)
+    pol.train()
+    agent = PPO(pol, c.ppo.clip_param, ep, 1, c.ppo.value_loss_coef, c.ppo.entropy_coef, lr=c.training.lr,
+                eps=c.training.eps, max_grad_norm=c.training.max_grad_norm)
+    tr = RolloutTrainer(c, envs, pol, agent, deterministic=True)
+    torch.manual_seed(99)
+    st = tr.update()
+    r = tr.rollouts
+    np.testing.assert_allclose(r.actions.cpu().numpy(), z["action"], atol=5e-5, rtol=0)
+    np.testing.assert_allclose(r.value_preds[:Tn].cpu().numpy(), z["value"], atol=5e-5, rtol=1e-5)
+    np.testing.assert_allclose(r.rewards.cpu().numpy(), z["reward"], atol=2e-4, rtol=0)
+    np.testing.assert_array_equal((r.masks[1:].cpu().numpy()[..., 0] == 0).astype(np.uint8), z["done"])
+    np.testing.assert_allclose(r.returns[:Tn].cpu().numpy(), z["returns"][:Tn], atol=2e-4, rtol=0)
+    np.testing.assert_allclose([st["value_loss"], st["action_loss"], st["dist_entropy"]], z["update_losses"],
+                               rtol=1e-3, atol=1e-5)
+    assert st["episodes"] == int(z["done"].sum())
+    for k, v in pol.state_dict().items():
+        np.testing.assert_allclose(v.cpu().numpy(), z["param_" + k], atol=2e-5, rtol=0, err_msg=k)
+    # train.py:216-222: with use_linear_lr_decay the lr of update j is lr * (1 - j / num_updates)
+    c.training.use_linear_lr_decay = True
+    tr.update_index = 1
+    tr.num_updates = 4
+    tr.update()
+    assert abs(agent.optimizer.param_groups[0]["lr"] - c.training.lr * 0.75) < 1e-12
+    envs.close()
