@@ -183,6 +183,16 @@ __device__ inline bool in_fov(double fx, double fy, double px1, double py1, doub
     return fabs(acos(d)) <= fov / 2;
 }
 
+// the robot's FOV test of a freshly spawned human (generate_ob(reset=True)), out of line: inlined into the
+// step kernel's RNG phase, the acos polynomial's f64 constants were hoisted to the loop preheader and
+// spilled to scratch by every wave with RNG work; only FOV < 2 pi configurations call it
+__device__ __noinline__ int reset_fov_test(double th, double rpx, double rpy, double px, double py, double fov)
+{
+    double fx, fy;
+    fov_dir64(th, fx, fy);
+    return in_fov(fx, fy, rpx, rpy, px, py, fov) ? 1 : 0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // shapely restatements (parity unpinned)
 // ------------------------------------------------------------------------------------------------
@@ -1071,11 +1081,7 @@ __device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &
         // generate_ob(reset=True): robot velocity is 0 (ints) -> float64 FOV path
         const double th0 = c.kinematics == CN_HOLONOMIC ? 0.0 : rth;   // atan2(0, 0) = 0
         int v = c.robot_fov >= 2.0 * CN_PI ? vis360(isfinite(th0), rpx, rpy, px, py) : -1;
-        if (v < 0) {
-            double fx, fy;
-            fov_dir64(c.kinematics == CN_HOLONOMIC ? atan2(0.0, 0.0) : rth, fx, fy);
-            v = in_fov(fx, fy, rpx, rpy, px, py, c.robot_fov) ? 1 : 0;
-        }
+        if (v < 0) v = reset_fov_test(th0, rpx, rpy, px, py, c.robot_fov);
         double bpx, bpy, bvx, bvy, br;
         if (v) { bpx = px; bpy = py; bvx = 0; bvy = 0; br = en.hr[lane]; }
         else { bpx = 15.0; bpy = 15.0; bvx = 0.0; bvy = 0.0; br = 0.3; }
@@ -1481,7 +1487,13 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     const cn_state_ptrs &S = g.s;
 
     const int tid = threadIdx.x;
-    const int e0 = blockIdx.x * EPB;
+    // XCD-aware env placement: workgroup i runs on XCD i % 8 (round-robin dispatch; for speed only), so
+    // give each XCD a contiguous run of env blocks. Neighbouring workgroups share the 128-B lines at the
+    // ends of their SoA segments (a per-env field of one workgroup is only 48 B); on one XCD the second
+    // reader hits in that XCD's L2 instead of fetching the line again.
+    const int nbk = g.pend.step_blocks, xq = nbk >> 3, xr = nbk & 7, xi = (int)blockIdx.x & 7;
+    const int blk = xi * xq + min(xi, xr) + ((int)blockIdx.x >> 3);
+    const int e0 = blk * EPB;
     const int nenv_here = min(EPB, g.E - e0);
     const int el = tid / N, i = tid - el * N;
     const bool hl = el < nenv_here;               // human lane
@@ -2018,22 +2030,24 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const float a0 = sl.act[re], a1 = sl.act[EPB + re];
         const int eb = re * N;
         double dmin = INFINITY;
-        bool collision = false, nz_viol = false, nz_checked = false;
+        bool collision = false, nz_viol = false;
         int vr_viol = 0, agg = 0;
         for (int k = 0; k < N; ++k) {
             const double cd = sl.cd[eb + k];
             if (cd < 0) { collision = true; break; }
             else if (cd < dmin) dmin = cd;
-            if (c.norm_zones && !nz_checked) {
-                nz_checked = true;
-                nz_viol = robot_norm_zone_violation(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB),
-                                                    RF(sl, R_VY, re, EPB), rr, (flags & CN_FLAG_ROBOT_F32) != 0,
-                                                    c.norm_zone_lhs);
-            }
             const uint32_t f = sl.lf[eb + k];
             vr_viol += (f & LF_VR) ? 1 : 0;
             agg += (f & LF_NOTREACHED) ? 1 : 0;
         }
+        // the reference tests the norm zones inside the loop once human 0 is not a collision; the penalty
+        // is read only on the no-collision branch of the ladder, where the loop ran past human 0, so
+        // testing it here (outside the loop: the call's register saves only run when it is taken) is
+        // the same
+        if (c.norm_zones && !collision)
+            nz_viol = robot_norm_zone_violation(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB),
+                                                RF(sl, R_VY, re, EPB), rr, (flags & CN_FLAG_ROBOT_F32) != 0,
+                                                c.norm_zone_lhs);
         const uint32_t bits = (uint32_t)RF(sl, R_BITS, re, EPB);
         const bool reaching_goal = (bits & 1u) != 0, inside = (bits & 2u) != 0;
         if (!reaching_goal) ++agg;
@@ -2178,6 +2192,15 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         double *hb = (double *)(wb + 2 * CN_MT_N * 4);
         ResetOut o;
         o.s = S; o.robot_node = g.robot_node; o.temporal = g.temporal; o.spatial = g.spatial; o.case_size = g.case_size;
+        // waves without an env to serve skip the block entirely: the loop's preheader (values the
+        // compiler hoists out of the RNG work, and their spill stores) then runs only where it is needed
+        bool mine = false;
+        {
+            int jj = 0;
+            for (int q = 0; q < nenv_here; ++q)
+                if (sl.rflag[EPB + q] & 7u) mine |= (jj++ % nw) == w;
+        }
+        if (mine) {
         int j = 0;
         for (int q = 0; q < nenv_here; ++q) {
             const uint32_t need = sl.rflag[EPB + q] & 7u;
@@ -2203,6 +2226,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 // land within reach of its own human), so it runs whenever end goal changing is on
                 goal_changes(c, S, e, en, m, (need & 2u) != 0, c.end_goal_changing != 0, hb);
             }
+        }
         }
     }
 #ifdef CN_STAMPS
@@ -2478,6 +2502,14 @@ __global__ void __launch_bounds__(64) cn_disc_quad_kernel(int64_t n, int mode, c
     if (i >= n) return;
     out[i] = mode ? disc_quad_sat(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i)
                   : disc_quad_intersect(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i);
+}
+
+// cn_debug_copy64: one wave per segment of `seg` doubles
+__global__ void __launch_bounds__(64) cn_copy64_kernel(int64_t n, int seg, const double *__restrict__ src,
+                                                       double *__restrict__ dst)
+{
+    const int64_t k = (int64_t)blockIdx.x * seg + threadIdx.x;
+    if ((int)threadIdx.x < seg && k < n) dst[k] = src[k];
 }
 
 // cn_debug_orca: one quad per simulator (16 per 64-lane workgroup), the step kernel's quad-path functions
@@ -2834,6 +2866,15 @@ int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, cons
     if (n <= 0 || !px || !py || !r || !qx || !qy || !out) return set_err(CN_EINVAL, "cn_debug_disc_quad: n > 0 and buffers required");
     hipLaunchKernelGGL(cn_disc_quad_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, n, mode,
                        px, py, r, qx, qy, out);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
+
+int cn_debug_copy64(void *stream, int64_t n, int seg, const double *src, double *dst)
+{
+    if (n <= 0 || seg < 1 || seg > 64 || !src || !dst) return set_err(CN_EINVAL, "cn_debug_copy64: n > 0, 1 <= seg <= 64");
+    hipLaunchKernelGGL(cn_copy64_kernel, dim3((unsigned)((n + seg - 1) / seg)), dim3(64), 0, (hipStream_t)stream, n, seg,
+                       src, dst);
     HIPCHK(hipGetLastError());
     return CN_OK;
 }

@@ -244,6 +244,13 @@ int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, cons
 int cn_debug_orca(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
                   float time_horizon, float time_step, float *out);
 
+/* Profiler calibration hook (MI355X_MICROARCH.md § HBM: FETCH_SIZE / WRITE_SIZE are calibrated only for
+ * 16-B-per-lane streams): dst[k] = src[k] over n doubles with the step kernel's access shape, one 8-B load
+ * and store per lane, in segments of `seg` consecutive doubles per 64-lane wave (seg = 64: a field of the
+ * per-human SoA arrays; seg = 6: a per-env field of one workgroup). tools/calib_pmc.py reads the
+ * counters of known byte counts through it. */
+int cn_debug_copy64(void *stream, int64_t n, int seg, const double *src, double *dst);
+
 /* out[r][h] = sum_n hs[r][n][h] * attn[r][n]; hs [R][N][H], attn [R][N], out [R][H]; H % 4 == 0. */
 int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, float *out);
 

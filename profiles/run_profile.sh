@@ -26,4 +26,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/write -o write --output-
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -T -d $OUT/sq1 -o sq1 --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_sq1.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_SMEM SQ_INSTS_VSKIPPED -T -d $OUT/sq2 -o sq2 --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_sq2.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum -T -d $OUT/tcc -o tcc --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench_tcc.log 2>&1
+# calibration of FETCH_SIZE / WRITE_SIZE on this kernel's 8-B-per-lane access shape (tools/calib_pmc.py)
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/calfetch -o calfetch --output-format csv -- python3 $R/tools/calib_pmc.py > $OUT/calib_fetch.log 2>&1
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -T -d $OUT/calwrite -o calwrite --output-format csv -- python3 $R/tools/calib_pmc.py > $OUT/calib_write.log 2>&1
 echo profile $TAG done

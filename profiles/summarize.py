@@ -7,10 +7,14 @@ profiles/pmc_<tag>.json (per kernel: average duration, counters per launch, deri
 records the library's CN_SRC_HASH (cn_version() on the box): bench.py takes `roofline.traffic` from
 the newest pmc_*.json whose hash equals the hash of the sources it runs, and reports null otherwise.
 
-HBM bytes follow MI355X_MICROARCH.md § HBM: FETCH_SIZE / WRITE_SIZE are KiB; on gfx950 FETCH_SIZE
-reports 1/2 of the bytes of wide coalesced streaming reads, so the read side is doubled (calibrated for
-16-B-per-lane streaming loads; this kernel's loads are 8 B per lane, so the absolute read figure carries
-that caveat). Infinity-Cache hits are counted as fabric traffic by these counters.
+HBM bytes follow MI355X_MICROARCH.md § HBM: FETCH_SIZE / WRITE_SIZE are KiB, and on gfx950 FETCH_SIZE
+reports 1/2 of the bytes of wide 16-B-per-lane streaming reads; other access widths "are uncalibrated:
+calibrate on a known byte count in your own access pattern". The step kernel's accesses are 8 B per lane,
+so run_profile.sh also profiles tools/calib_pmc.py (cn_debug_copy64: a known byte count moved with that
+shape, as full 64-lane segments and as 48-B per-env segments); the counters are divided by the
+calibration's bytes-per-counted-byte of the full-segment shape (`calibration` in the JSON) and both the
+guide's 16-B correction (x2 on FETCH) and the calibrated figure are recorded; `hbm_bytes_per_launch` is
+the calibrated one when a calibration is present. Infinity-Cache hits count as fabric traffic here.
 VALU-issue fraction = SQ_INSTS_VALU x 2 cycles (one wave64 VALU instruction occupies a SIMD's issue for
 2 cycles; f64 FMA/MUL/ADD take 4, transcendentals 8 on f64 per the microarchitecture guide's
 issue-cost table) / (1024 SIMDs x kernel cycles at 2.4 GHz).
@@ -77,6 +81,17 @@ def main():
         for k, cs in counters(find(os.path.join(out, p), "*counter_collection.csv")).items():
             for c, v in cs.items():
                 merged.setdefault(k, {})[c] = sum(v) / len(v)
+    cal = {}
+    for p, cname in (("calfetch", "FETCH_SIZE"), ("calwrite", "WRITE_SIZE")):
+        for k, cs in counters(find(os.path.join(out, p), "*counter_collection.csv")).items():
+            if "copy64" in k and cname in cs:
+                v = cs[cname]
+                h = len(v) // 2
+                nbytes = float(8 << 23)   # tools/calib_pmc.py: 8 M doubles each way
+                cal[cname] = {"seg64": sum(v[:h]) / h * 1024.0 / nbytes, "seg6": sum(v[h:]) / (len(v) - h) * 1024.0 / nbytes}
+    if cal:
+        lines.append("calibration (counted bytes / moved bytes, cn_debug_copy64, 8 B per lane): %s" % json.dumps(cal))
+        lines.append("")
     lines.append("")
     lines.append("counters per launch (mean over dispatches)")
     for k in sorted(merged):
@@ -87,8 +102,17 @@ def main():
         for n in sorted(c):
             lines.append("    %-28s %.6g" % (n, c[n]))
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            d["hbm_bytes_per_launch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
-            lines.append("    => HBM bytes/launch (2*FETCH_SIZE + WRITE_SIZE) = %.0f" % d["hbm_bytes_per_launch"])
+            d["hbm_bytes_guide_16B"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+            d["hbm_bytes_per_launch"] = d["hbm_bytes_guide_16B"]
+            lines.append("    => HBM bytes/launch, guide's 16-B correction (2*FETCH_SIZE + WRITE_SIZE) = %.0f"
+                         % d["hbm_bytes_guide_16B"])
+            if "FETCH_SIZE" in cal and "WRITE_SIZE" in cal:
+                rd = c["FETCH_SIZE"] * 1024.0 / cal["FETCH_SIZE"]["seg64"]
+                wr = c["WRITE_SIZE"] * 1024.0 / cal["WRITE_SIZE"]["seg64"]
+                d["hbm_read_bytes"], d["hbm_write_bytes"] = rd, wr
+                d["hbm_bytes_per_launch"] = rd + wr
+                lines.append("    => HBM bytes/launch, calibrated on the 8-B shape: read %.0f + write %.0f = %.0f"
+                             % (rd, wr, rd + wr))
         dur = d.get("avg_duration_ns")
         if dur and "SQ_INSTS_VALU" in c:
             cyc = dur * 1e-9 * CLOCK_HZ
@@ -100,7 +124,8 @@ def main():
             d["wait_any_frac"] = c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"]
             lines.append("    => per-wave: issuing %.3f, parked on waitcnt/barrier %.3f of wave cycles" % (
                 d["active_inst_frac"], d["wait_any_frac"]))
-    doc = {"tag": tag, "bench_args": args, "lib_version": ver, "lib_src_hash": src_hash, "kernels": res}
+    doc = {"tag": tag, "bench_args": args, "lib_version": ver, "lib_src_hash": src_hash, "calibration": cal,
+           "kernels": res}
     json.dump(doc, open(os.path.join(HERE, "pmc_%s.json" % tag), "w"), indent=1)
     open(os.path.join(HERE, "%s_summary.txt" % tag), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))

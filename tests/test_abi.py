@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     txt = open(os.path.join(REPO, "include", "crowdnav.h")).read()
-    return sorted(set(re.findall(r"\b(cn_[a-z_]+)\s*\(", txt)) - {"cn_engine"})
+    return sorted(set(re.findall(r"\b(cn_[a-z_0-9]+)\s*\(", txt)) - {"cn_engine"})
 
 
 @pytest.fixture(scope="module")
