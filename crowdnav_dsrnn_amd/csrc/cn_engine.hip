@@ -42,6 +42,7 @@ __device__ __forceinline__ void wsync()
 #define CN_NSTAMP 16
 __device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
+__device__ unsigned long long cn_stamp_c[8192 * 4];   // crowded rejection: ensure / cand / test / passes
 #define STAMP_A(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + (k)] = clock64(); } while (0)
 #define STAMP_B(w, k) do { if ((threadIdx.x & 63) == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
 #else
@@ -64,12 +65,15 @@ struct StepPlan {
     // LDS byte offsets
     int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_vis, o_nv, o_lines, o_proj, o_nd, o_ns, o_perm,
         total;
-    int rng_waves;   // phase-5 RNG regions (CN_PEND_LDS each), laid over o_lines
+    int rng_waves;   // phase-5 RNG regions (rng_stride bytes each), laid over o_lines
+    int rng_stride;  // CN_PEND_LDS, + CN_GRID_LDS when the plan has room for the spawn's DiscGrid
 };
 
 #define CN_RENV_F 27   // robot/env doubles per env in LDS
 #define CN_HUM_F 14    // human doubles per lane in LDS
 #define CN_PEND_LDS (2 * CN_MT_N * 4 + 7 * 32 * 8 + 6 * 64 * 8)   // per RNG wave: MT ring, agent table, try slots
+#define CN_GRID 16
+#define CN_GRID_LDS (96 * 8 + CN_GRID * CN_GRID * 4 + 4 * 8 + 4 * 8)   // + spawn DiscGrid: agent table, masks, cover, box
 
 __host__ __device__ inline int cn_align16(int x) { return (x + 15) & ~15; }
 
@@ -105,7 +109,10 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * H : 0));
     p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * H : 0));
     p.rng_waves = 4;
-    const int rng_end = p.o_lines + p.rng_waves * CN_PEND_LDS;
+    // the DiscGrid region only where it costs no LDS (the kd-tree path's ORCA scratch is larger than the
+    // RNG regions it hosts); the quad path keeps its 3 workgroups per CU
+    p.rng_stride = p.o_lines + p.rng_waves * (CN_PEND_LDS + CN_GRID_LDS) <= o ? CN_PEND_LDS + CN_GRID_LDS : CN_PEND_LDS;
+    const int rng_end = p.o_lines + p.rng_waves * p.rng_stride;
     p.total = o > rng_end ? o : rng_end;
     return p;
 }
@@ -676,6 +683,9 @@ __device__ __forceinline__ int orca_lines_quad(const SlotF &slot, int M, int sq,
 // reset has run, so the spawn of env e's NEXT episode is drawn ahead of time by spare waves of kernel A
 // (off the critical path) and kernel B's auto-reset only copies it. (case_counter, reset_count) is
 // the validity key: a stale entry (e.g. after cn_set_state) is never used, the reset is then drawn inline.
+// Two slots per env (slot = reset_count & 1): the spawn of the env's next reset and of the one after, so
+// an env that ends an episode one step after a reset (common where spawns overlap, e.g. 25 humans in
+// square_crossing) finds its spawn drawn instead of drawing it inline. Arrays are [2][...].
 struct PendPtrs {
     uint32_t *mt;   // [E][624] key words after the spawn draws
     int32_t *pos;   // [E] stream position
@@ -687,6 +697,13 @@ struct PendPtrs {
     double *r;      // [5][E] robot px, py, gx, gy, theta
     double *h;      // [7][E*N] human px, py, gx, gy, radius, v_pref, theta
 };
+__host__ __device__ inline PendPtrs pend_slot(const PendPtrs &P, int s, int64_t E, int64_t EN)
+{
+    PendPtrs q = P;
+    q.mt += s * E * CN_MT_N; q.pos += s * E; q.ovf += s * E; q.sc += s * E; q.cc += s * E; q.rc += s * E;
+    q.ok += s * E; q.r += s * 5 * E; q.h += s * 7 * EN;
+    return q;
+}
 
 // where a reset writes: state + the first observation of the new episode
 struct ResetOut {
@@ -708,18 +725,40 @@ struct RngArgs {   // cn_reset_kernel
 // "sequential" draws are read by all lanes (LDS broadcast), and rejection loops evaluate up to 64
 // consecutive tries speculatively, one per lane, since each try consumes a fixed number of words.
 
-// wave-cooperative mt19937_gen: n = gen(o) (all 64 lanes of the workgroup must call it)
-__device__ inline void mt_gen_wave(const uint32_t *o, uint32_t *n, int lane)
+// wave-cooperative mt19937_gen: n = gen(o) (all 64 lanes of the workgroup must call it). Three
+// sections, each with all its LDS loads issued before its stores: new[k] for k < 227 needs old words
+// only; k in [227, 454) needs new[k - 227] of the first section, k in [454, 624) new words of the second
+// (k = 623 wraps to new[0], and its new[396] is second-section too).
+__device__ __forceinline__ void mt_gen_wave_inl(const uint32_t *__restrict__ o, uint32_t *__restrict__ n, int lane)
 {
-    for (int k = lane; k < CN_MT_N - 397; k += 64) n[k] = mt_mix(o[k], o[k + 1], o[k + 397]);
-    wsync();
-    for (int base = CN_MT_N - 397; base < CN_MT_N - 1; base += 227) {
-        const int end = min(base + 227, CN_MT_N - 1);
-        for (int k = base + lane; k < end; k += 64) n[k] = mt_mix(o[k], o[k + 1], n[k + (397 - CN_MT_N)]);
+    constexpr int S = CN_MT_N - 397;   // 227
+#pragma unroll
+    for (int sec = 0; sec < 3; ++sec) {
+        const int lo = sec * S, hi = sec == 2 ? CN_MT_N : (sec + 1) * S;
+        uint32_t a[4], b[4], cc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = lo + lane + 64 * j;
+            if (k < hi) {
+                a[j] = o[k];
+                b[j] = k + 1 < CN_MT_N ? o[k + 1] : n[0];
+                cc[j] = sec == 0 ? o[k + 397] : n[k - S];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = lo + lane + 64 * j;
+            if (k < hi) n[k] = mt_mix(a[j], b[j], cc[j]);
+        }
         wsync();
     }
-    if (lane == 0) n[CN_MT_N - 1] = mt_mix(o[CN_MT_N - 1], n[0], n[396]);
-    wsync();
+}
+
+// out of line for the many rarely-taken call sites (inlined everywhere, the step kernel's code grew by
+// half and ran slower); the crowded rejection loop, which twists a block per pass, inlines it
+__device__ __noinline__ void mt_gen_wave(const uint32_t *__restrict__ o, uint32_t *__restrict__ n, int lane)
+{
+    mt_gen_wave_inl(o, n, lane);
 }
 
 __device__ __forceinline__ double mt_dbl(const uint32_t *w, int q)
@@ -727,31 +766,49 @@ __device__ __forceinline__ double mt_dbl(const uint32_t *w, int q)
     const int32_t a = (int32_t)(mt_temper(w[q]) >> 5), b = (int32_t)(mt_temper(w[q + 1]) >> 6);
     return (a * 67108864.0 + b) / 9007199254740992.0;
 }
+// the same over the ping-pong ring: logical word q lives at (q + off) mod 2*624
+__device__ __forceinline__ double mt_dbl_ring(const uint32_t *w, int q, int off)
+{
+    int i = q + off;
+    i -= i >= 2 * CN_MT_N ? 2 * CN_MT_N : 0;
+    const int i1 = i + 1 == 2 * CN_MT_N ? 0 : i + 1;
+    const int32_t a = (int32_t)(mt_temper(w[i]) >> 5), b = (int32_t)(mt_temper(w[i1]) >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
 
 // CN_RNG_PHILOX (`phx`): word q is philox(q >> 2) under the episode key (`key`, also kept in w[0] for the
 // state write-back); the ring is unused, p counts words from the reset and ensure() is a no-op.
 struct WRng {
     double *sl;    // LDS [6][64] per-try candidate slots (wave_reject2)
-    uint32_t *w;   // LDS [2*624]
+    uint32_t *w;   // LDS [2*624], a ping-pong ring: logical block 0 (the key) starts at word `off`
+    int off;       // 0 or 624
     int p;         // stream position (wave-uniform), 0 .. 2*624 (MT19937) / words since the reset (Philox)
     bool have1;    // block 1 generated
     bool slid;     // the key advanced by at least one whole block (key words must be written back)
     bool phx;      // CN_RNG_PHILOX
+    int64_t edbg;  // env index for the -DCN_STAMPS diagnostics
+    char *grid;    // CN_GRID_LDS bytes of LDS for the spawn's crowded rejection (DiscGrid + agent table), or null
     uint32_t key;  // Philox key word 0 (the episode seed)
     int lane;
-    __device__ double dbl(int q) const { return phx ? philox_dbl(key, q) : mt_dbl(w, q); }
+    __device__ double dbl(int q) const { return phx ? philox_dbl(key, q) : mt_dbl_ring(w, q, off); }
+    // logical block i (0 = the key, 1 = the key after the next mt19937_gen)
+    __device__ uint32_t *blk(int i) const { return w + ((off + i * CN_MT_N) % (2 * CN_MT_N)); }
     // R * cos(angle) with angle = rnd() * pi * 2 (crowd_sim.py:361, 736), for cand_attributes
     __device__ double cos2pi(int q) const { return cos(dbl(q) * CN_PI * 2); }
     __device__ double sin2pi(int q) const { return sin(dbl(q) * CN_PI * 2); }
     // make words [p, p + need) readable (need <= 624); all lanes call it together
+    template <bool INL = false>
     __device__ void ensure(int need)
     {
         if (phx) return;
-        if (p + need > CN_MT_N && !have1) { mt_gen_wave(w, w + CN_MT_N, lane); have1 = true; }
-        if (p + need > 2 * CN_MT_N) {
-            for (int k = lane; k < CN_MT_N; k += 64) w[k] = w[CN_MT_N + k];
+        if (p + need > CN_MT_N && !have1) {
+            if (INL) mt_gen_wave_inl(blk(0), blk(1), lane); else mt_gen_wave(blk(0), blk(1), lane);
+            have1 = true;
+        }
+        if (p + need > 2 * CN_MT_N) {   // slide: block 1 becomes the key, the next block overwrites block 0
             wsync();
-            mt_gen_wave(w, w + CN_MT_N, lane);
+            off = off ? 0 : CN_MT_N;
+            if (INL) mt_gen_wave_inl(blk(0), blk(1), lane); else mt_gen_wave(blk(0), blk(1), lane);
             p -= CN_MT_N;
             slid = true;
         }
@@ -898,6 +955,158 @@ __device__ int wave_reject2(WRng &m, int W, int NA, int max_tries, uint32_t &ovf
     }
 }
 
+// Binned disc test for the crowded passes of the spawn's rejection loops (wave_reject_discs): a try is
+// rejected iff its point lies strictly inside one of the agents' discs; the discs except agent 0's (the
+// robot, often far from the crowd, tested exactly) are binned once per call into a 16 x 16 grid over their
+// bounding box (4 cells per lane, float32 with a 1e-4 m margin, so the binning is conservative): a cell
+// lying inside some disc rejects every try that lands in it, a try outside the box hits nothing, and
+// otherwise only the agents overlapping its cell are tested exactly (norm_lt). Same result as testing
+// every agent. (The goal rejection keeps the plain test: binning there measured no gain in C3 and cost
+// the quad path 8 % in code size.)
+struct DiscGrid {
+    uint32_t *mask;   // [256] per cell: bit a = agent a's position or goal disc overlaps the cell (NA <= 32)
+    uint64_t *cov;    // [4] bit = cell entirely inside some disc
+    double *par;      // x0, y0, 16 / width, 16 / height
+};
+
+template <bool GOALS = true>
+__device__ __forceinline__ void disc_grid_build(const DiscGrid &gr, const double *tx, const double *ty, const double *tgx,
+                                                const double *tgy, const double *tmd, int NA, int lane)
+{
+    // bounding box of every disc (wave-uniform: each lane scans the table)
+    // agent 0 (the robot, often far from the crowd) stays out of the grid: disc_grid_hit tests it exactly
+    double x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY;
+    for (int a = 1; a < NA; ++a) {
+        const double d = tmd[a] + 1e-3;
+        const double ax = tx[a], ay = ty[a], bx = GOALS ? tgx[a] : ax, by = GOALS ? tgy[a] : ay;
+        x0 = fmin(x0, fmin(ax, bx) - d); x1 = fmax(x1, fmax(ax, bx) + d);
+        y0 = fmin(y0, fmin(ay, by) - d); y1 = fmax(y1, fmax(ay, by) + d);
+    }
+    const double ivx = CN_GRID / (x1 - x0), ivy = CN_GRID / (y1 - y0);
+    // cells lane + 64 j (j < 4): column lane & 15, row 4 j + lane / 16; each expanded by 1e-4 m (a try is
+    // binned in double precision; near a cell edge it may land in the neighbour, which the expansion covers)
+    const float m = 1e-4f;
+    const int ix = lane & 15;
+    const float cx0 = (float)(x0 + ix / ivx) - m, cx1 = (float)(x0 + (ix + 1) / ivx) + m;
+    float cy0[4], cy1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int iy = 4 * j + (lane >> 4);
+        cy0[j] = (float)(y0 + iy / ivy) - m; cy1[j] = (float)(y0 + (iy + 1) / ivy) + m;
+    }
+    uint32_t msk[4] = {0u, 0u, 0u, 0u};
+    bool covered[4] = {false, false, false, false};
+    for (int a = 1; a < NA; ++a) {
+        const float d = (float)tmd[a], dl = d + m, ds = d - m;
+#pragma unroll
+        for (int g = 0; g < (GOALS ? 2 : 1); ++g) {
+            const float px = (float)(g ? tgx[a] : tx[a]), py = (float)(g ? tgy[a] : ty[a]);
+            const float nx = fmaxf(0.0f, fmaxf(cx0 - px, px - cx1));
+            const float fx = fmaxf(fabsf(px - cx0), fabsf(px - cx1));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float ny = fmaxf(0.0f, fmaxf(cy0[j] - py, py - cy1[j]));
+                const float fy = fmaxf(fabsf(py - cy0[j]), fabsf(py - cy1[j]));
+                if (nx * nx + ny * ny <= dl * dl) msk[j] |= 1u << a;
+                if (ds > 0.0f && fx * fx + fy * fy < ds * ds) covered[j] = true;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        gr.mask[lane + 64 * j] = msk[j];
+        const uint64_t cv = __ballot(covered[j]);
+        if (lane == 0) gr.cov[j] = cv;
+    }
+    if (lane == 0) { gr.par[0] = x0; gr.par[1] = y0; gr.par[2] = ivx; gr.par[3] = ivy; }
+}
+
+// does the goal (gx, gy) lie strictly inside one of the discs? Exact tests (norm_lt) of the agents
+// binned in its cell, two agents (four discs) per round with their loads issued together
+template <bool GOALS = true>
+__device__ __forceinline__ bool disc_grid_hit(const DiscGrid &gr, const double *tx, const double *ty, const double *tgx,
+                                              const double *tgy, const double *tmd, double gx, double gy)
+{
+    if (norm_lt(gx - tx[0], gy - ty[0], tmd[0]) || (GOALS && norm_lt(gx - tgx[0], gy - tgy[0], tmd[0]))) return true;
+    const double fx = (gx - gr.par[0]) * gr.par[2], fy = (gy - gr.par[1]) * gr.par[3];
+    if (!(fx >= 0.0 && fx < CN_GRID && fy >= 0.0 && fy < CN_GRID)) return false;   // outside every other disc
+    const int cell = (int)fy * CN_GRID + (int)fx;
+    if ((gr.cov[cell >> 6] >> (cell & 63)) & 1ull) return true;
+    uint32_t msk = gr.mask[cell];
+    bool hit = false;
+    while (msk && !hit) {
+        const int a0 = __ffs(msk) - 1;
+        msk &= msk - 1;
+        const int a1 = msk ? __ffs(msk) - 1 : a0;
+        msk &= msk - 1;
+        const double x0 = tx[a0], y0 = ty[a0], d0 = tmd[a0];
+        const double x1 = tx[a1], y1 = ty[a1], d1 = tmd[a1];
+        hit = norm_lt(gx - x0, gy - y0, d0) | norm_lt(gx - x1, gy - y1, d1);
+        if (GOALS) {
+            const double u0 = tgx[a0], v0 = tgy[a0], u1 = tgx[a1], v1 = tgy[a1];
+            hit = hit | norm_lt(gx - u0, gy - v0, d0) | norm_lt(gx - u1, gy - v1, d1);
+        }
+    }
+    return hit;
+}
+
+// wave_reject2 for "the candidate point (m.sl[t], m.sl[64 + t]) lies strictly inside one of NA discs"
+// (`disc(a, x, y, md)`: centre and radius of agent a): the spawn's human placement (crowd_sim.py:369-390).
+// When the wave has grid space (m.grid) the crowded passes bin the discs once into a DiscGrid (see
+// goal_reject_crowded) and test each try against its cell's agents only; same result.
+template <bool GRID, typename FC, typename FD>
+__device__ int wave_reject_discs(WRng &m, int W, int NA, int max_tries, uint32_t &ovf, FC cand, FD disc)
+{
+    auto hit = [&](int t, int a) {
+        double x, y, md;
+        disc(a, x, y, md);
+        return norm_lt(m.sl[t] - x, m.sl[64 + t] - y, md);
+    };
+    if (!GRID || !m.grid || NA < 8) return wave_reject2(m, W, NA, max_tries, ovf, cand, hit);
+    const int lane = m.lane;
+    const uint64_t gmask = NA >= 64 ? ~0ull : ((1ull << NA) - 1ull);
+    int t0 = 0;
+    {   // first pass, lane = (try, agent), as wave_reject2
+        const int J = min(64 / NA, CN_MT_N / W);
+        const int t = lane / NA, a = lane - t * NA;
+        m.ensure(W * J);
+        const int nt = min(J, max_tries);
+        const bool valid = t < nt;
+        if (valid && a == 0) cand(m.p + W * t, t);
+        wsync();
+        const uint64_t badm = __ballot(valid && hit(t, a));
+        for (int k = 0; k < nt; ++k)
+            if (((badm >> (k * NA)) & gmask) == 0) { m.p += W * (k + 1); return k; }
+        if (J >= max_tries) { m.p += W * nt; ++ovf; return nt - 1; }
+        m.p += W * J;
+        t0 = J;
+    }
+    double *tx = (double *)m.grid, *ty = tx + 32, *tmd = tx + 64;
+    DiscGrid gr;
+    gr.mask = (uint32_t *)(tx + 96); gr.cov = (uint64_t *)(tx + 96 + CN_GRID * CN_GRID / 2); gr.par = (double *)(gr.cov + 4);
+    if (lane < NA) { double x, y, md; disc(lane, x, y, md); tx[lane] = x; ty[lane] = y; tmd[lane] = md; }
+    wsync();
+    disc_grid_build<false>(gr, tx, ty, tx, ty, tmd, NA, lane);
+    const int J = min(64, CN_MT_N / W);
+    for (;; t0 += J) {
+        m.template ensure<true>(W * J);
+        const int nt = min(J, max_tries - t0);
+        const bool valid = lane < nt;
+        if (valid) cand(m.p + W * lane, lane);
+        wsync();
+        const bool bad = !valid || disc_grid_hit<false>(gr, tx, ty, tx, ty, tmd, m.sl[lane], m.sl[64 + lane]);
+        const uint64_t okm = __ballot(!bad);
+        if (okm) {
+            const int first = __ffsll((long long)okm) - 1;
+            m.p += W * (first + 1);
+            return first;
+        }
+        if (t0 + J >= max_tries) { m.p += W * nt; ++ovf; return nt - 1; }
+        m.p += W * J;
+        wsync();   // slots are rewritten by the next pass
+    }
+}
+
 // Crowded goal rejection (a goal pass whose first batch was all rejected; in square_crossing at N = 25
 // most of these loops run to max_tries): one try per lane, 64 at a time, straight from the stream; the
 // agents (robot, then the other humans in index order) sit in an LDS table with their minimum distance
@@ -919,9 +1128,16 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
         }
         tmd[lane] = r_self + ar + c.discomfort_dist;
     }
+    wsync();
     const int J = min(64, CN_MT_N / W);
+#ifdef CN_STAMPS
+    unsigned long long tq = clock64(), tc_e = 0, tc_c = 0, tc_t = 0, tc_n = 0;
+#endif
     for (int t0 = 0;; t0 += J) {
-        m.ensure(W * J);
+        m.template ensure<true>(W * J);
+#ifdef CN_STAMPS
+        { const unsigned long long t_ = clock64(); tc_e += t_ - tq; tq = t_; ++tc_n; }
+#endif
         const int nt = min(J, max_tries - t0);
         double gx = 0, gy = 0;
         if (lane < nt) {
@@ -929,6 +1145,9 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
             gx = m.sl[lane]; gy = m.sl[64 + lane];
         }
         wsync();
+#ifdef CN_STAMPS
+        { const unsigned long long t_ = clock64(); tc_c += t_ - tq; tq = t_; }
+#endif
         bool bad = lane >= nt;
         for (int a0 = 0; a0 < NA && !bad; a0 += 4) {
             double x[4], y[4], u[4], v[4], d[4];
@@ -941,6 +1160,11 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
             for (int k = 0; k < 4; ++k)
                 bad = bad | norm_lt(gx - x[k], gy - y[k], d[k]) | norm_lt(gx - u[k], gy - v[k], d[k]);
         }
+#ifdef CN_STAMPS
+        { const uint64_t bb_ = __ballot(bad); (void)bb_; const unsigned long long t_ = clock64(); tc_t += t_ - tq; tq = t_;
+          if (lane == 0 && m.edbg >= 0 && m.edbg < 8192) { cn_stamp_c[m.edbg * 4] += tc_e; cn_stamp_c[m.edbg * 4 + 1] += tc_c; cn_stamp_c[m.edbg * 4 + 2] += tc_t; cn_stamp_c[m.edbg * 4 + 3] += 1; }
+          tc_e = tc_c = tc_t = 0; }
+#endif
         const uint64_t okm = __ballot(!bad);
         if (okm) {
             const int first = __ffsll((long long)okm) - 1;
@@ -957,12 +1181,14 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
 // crowd_sim.py:555-663; generate_circle_crossing_human :359-393): reseed the env's stream with
 // counter_offset + case_counter + thisSeed, draw the robot and then each human with rejection.
 // One wave; the result is left in `en` (LDS), rth, ovf, sc and the stream `m`.
+template <bool GRID>
 __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int64_t case_counter, int32_t reset_count,
                           int64_t counter_offset, WRng &m, Env1 &en, double &rth, uint32_t &ovf, int &sc)
 {
     const int lane = m.lane;
     const int N = c.human_num;
     uint32_t *mtw = m.w;
+    m.off = 0;   // a fresh stream: the key at the start of the ring
     if (c.scenario_mode == CN_SCMODE_SEQUENTIAL) sc = c.scenarios[reset_count % c.num_scenarios];
     else sc = c.scenarios[gidx % c.num_scenarios];
     const uint32_t seed0 = (uint32_t)(counter_offset + case_counter + (c.seed + gidx));
@@ -1012,13 +1238,12 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
         double vpref = c.human_vpref, rad = c.human_radius;
         if (c.randomize_attributes) { vpref = m.unif(0.5, 1.5); rad = m.unif(0.3, 0.5); }
         // candidate vs the robot and the humans placed so far (crowd_sim.py:369-390): i + 1 agent tests
-        const int tw = wave_reject2(m, W, i + 1, c.max_tries, ovf, [&](int q, int t) {
+        const int tw = wave_reject_discs<GRID>(m, W, i + 1, c.max_tries, ovf, [&](int q, int t) {
             double px, py, gx, gy, hd, vp;
             cand_attributes(c, m, q, sc, vpref, rad, en.rr, px, py, gx, gy, hd, vp);
             m.sl[t] = px; m.sl[64 + t] = py; m.sl[128 + t] = gx; m.sl[192 + t] = gy; m.sl[256 + t] = hd;
             m.sl[320 + t] = vp;
-        }, [&](int t, int a) {
-            double md, ax, ay;
+        }, [&](int a, double &ax, double &ay, double &md) {
             if (a == 0) {
                 ax = en.rpx; ay = en.rpy;
                 md = c.kinematics == CN_UNICYCLE ? R / 2 : rad + en.rr + c.discomfort_dist;
@@ -1026,7 +1251,6 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
                 ax = en.hpx[a - 1]; ay = en.hpy[a - 1];
                 md = rad + en.hr[a - 1] + c.discomfort_dist;
             }
-            return norm_lt(m.sl[t] - ax, m.sl[64 + t] - ay, md);
         });
         if (lane == 0) {
             en.hpx[i] = m.sl[tw]; en.hpy[i] = m.sl[64 + tw]; en.hgx[i] = m.sl[128 + tw]; en.hgy[i] = m.sl[192 + tw];
@@ -1036,11 +1260,12 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
     }
 }
 
-// Store a drawn spawn as env e's pending next episode.
-__device__ __forceinline__ void write_pending(const PendPtrs &P, const cn_config &c, int64_t E, int64_t e, const Env1 &en, double rth,
+// Store a drawn spawn as env e's pending episode for the reset with key (cc, rc), slot rc & 1.
+__device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_config &c, int64_t E, int64_t e, const Env1 &en, double rth,
                               int sc, uint32_t ovf, const uint32_t *mt_src, int pos, int64_t cc, int32_t rc, int lane)
 {
     const int N = c.human_num;
+    const PendPtrs P = pend_slot(P2, rc & 1, E, E * N);
     const int nk = c.rng_mode == CN_RNG_PHILOX ? 1 : CN_MT_N;   // key words to copy
     {
         uint32_t v[(CN_MT_N + 63) / 64];
@@ -1286,6 +1511,7 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
     const int lane = m.lane;
     uint32_t *mtw = m.w;
     const int64_t hb = e * N;
+    m.off = 0;
     if (m.phx) m.key = S.mt[e * CN_MT_N];
     else {
         uint32_t v[(CN_MT_N + 63) / 64];
@@ -1316,7 +1542,7 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
         S.h_r[hb + lane] = en.hr[lane]; S.h_vpref[hb + lane] = en.hvp[lane];
     }
     if (in1 || m.slid)
-        for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = mtw[(in1 ? CN_MT_N : 0) + k];
+        for (int k = lane; k < CN_MT_N; k += 64) S.mt[e * CN_MT_N + k] = m.blk(in1 ? 1 : 0)[k];
     if (lane == 0) { S.mt_pos[e] = in1 ? m.p - CN_MT_N : m.p; S.overflow[e] = ovf; }
     wsync();
     STAMP_B(e, 4);
@@ -1324,7 +1550,8 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
 
 // Auto-reset of env e (VecEnv worker, shmem_vec_env.py:164-168 -> CrowdSimDict.reset): copy the pending
 // spawn when `may_consume` and it is valid for the current key, else draw it here. One wave.
-__device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P, const cn_config &c, int64_t E, int64_t e,
+template <bool GRID>
+__device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2, const cn_config &c, int64_t E, int64_t e,
                           int64_t counter_offset, bool may_consume, WRng &m, Env1 &en)
 {
     const cn_state_ptrs &S = o.s;
@@ -1332,6 +1559,7 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P, 
     const int lane = m.lane;
     const int64_t cc = S.case_counter[e];
     const int32_t rc = S.reset_count[e];
+    const PendPtrs P = pend_slot(P2, rc & 1, E, E * N);
     if (may_consume && P.ok[e] && P.cc[e] == cc && P.rc[e] == rc) {
         if (lane < N) {
             const int64_t h = e * N + lane, EN = E * N;
@@ -1350,9 +1578,9 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P, 
         double rth;
         uint32_t ovf;
         int sc;
-        spawn_env(c, c.env_offset + e, cc, rc, counter_offset, m, en, rth, ovf, sc);
+        spawn_env<GRID>(c, c.env_offset + e, cc, rc, counter_offset, m, en, rth, ovf, sc);
         const bool in1 = !m.phx && m.p > CN_MT_N;
-        write_reset(o, c, e, en, rth, sc, ovf, m.w + (in1 ? CN_MT_N : 0), in1 ? m.p - CN_MT_N : m.p, lane);
+        write_reset(o, c, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, lane);
     }
     wsync();
 }
@@ -1366,34 +1594,42 @@ struct PendLaunch {
     int all;                // 1: every env (list ignored)
     int step_blocks, pend_blocks;
     int waves;              // spawning waves per spare workgroup (RNG regions that fit the launch's LDS)
+    int stride;             // bytes per spawning wave's region (StepPlan::rng_stride)
     int64_t counter_offset;
+    int64_t case_size;
 };
 
-template <bool PHX>
+// GRID: the spawn's crowded rejection through a DiscGrid (the kd-tree path's plans have LDS for it)
+template <bool PHX, bool GRID>
 __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_ptrs &S, const cn_config &c, int E, char *smem)
 {
     const int nw = pl.waves, w = threadIdx.x / 64, lane = threadIdx.x & 63;
     if (w >= nw) return;
-    char *base = smem + w * CN_PEND_LDS;
+    char *base = smem + w * pl.stride;
     uint32_t *mtw = (uint32_t *)base;
     double *hb = (double *)(base + 2 * CN_MT_N * 4);
-    const uint32_t n = pl.all ? (uint32_t)E : *pl.count;
+    // envs reset by the previous launch: the reset after next (the next one was drawn earlier); after
+    // cn_reset / cn_set_state (all): both the next (items [0, E)) and the one after ([E, 2E))
+    const uint32_t n = pl.all ? (uint32_t)(2 * E) : *pl.count;
     for (uint32_t it = (uint32_t)((blockIdx.x - pl.step_blocks) * nw + w); it < n; it += (uint32_t)(pl.pend_blocks * nw)) {
-        const int64_t e = pl.all ? (int64_t)it : (int64_t)pl.list[it];
+        const int64_t e = pl.all ? (int64_t)(it % (uint32_t)E) : (int64_t)pl.list[it];
+        const bool ahead2 = !pl.all || it >= (uint32_t)E;
         Env1 en;
         en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
         en.hth = hb + 192;
         WRng m;
-        m.w = mtw; m.lane = lane; m.phx = PHX;
+        m.w = mtw; m.off = 0; m.lane = lane; m.phx = PHX; m.edbg = -1;
+        m.grid = pl.stride > CN_PEND_LDS ? base + CN_PEND_LDS : nullptr;
         m.sl = (double *)(base + 2 * CN_MT_N * 4 + 7 * 32 * 8);
-        const int64_t cc = S.case_counter[e];
-        const int32_t rc = S.reset_count[e];
+        int64_t cc = S.case_counter[e];
+        int32_t rc = S.reset_count[e];
+        if (ahead2) { cc = (cc + c.nenv) % pl.case_size; rc += 1; }   // write_reset's counter update
         double rth;
         uint32_t ovf;
         int sc;
-        spawn_env(c, c.env_offset + e, cc, rc, pl.counter_offset, m, en, rth, ovf, sc);
+        spawn_env<GRID>(c, c.env_offset + e, cc, rc, pl.counter_offset, m, en, rth, ovf, sc);
         const bool in1 = !m.phx && m.p > CN_MT_N;
-        write_pending(pl.P, c, E, e, en, rth, sc, ovf, mtw + (in1 ? CN_MT_N : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
+        write_pending(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
                       lane);
         wsync();
     }
@@ -1458,7 +1694,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if ((int)blockIdx.x >= g.pend.step_blocks) {  // spare workgroups: draw upcoming episodes' spawns
-        pend_waves<PHX>(g.pend, g.s, c, g.E, smem);
+        pend_waves<PHX, KD>(g.pend, g.s, c, g.E, smem);
         return;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *g.pcount_zero = 0u;
@@ -2185,9 +2421,10 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     // spawn waves right now, so it (and every env after cn_reset/cn_set_state) draws inline instead.
     {
         const int nw = P.rng_waves, w = tid / 64, lane = tid & 63;
-        char *wb = smem + P.o_lines + (w < nw ? w : 0) * CN_PEND_LDS;   // over the ORCA scratch, dead after phase 2
+        char *wb = smem + P.o_lines + (w < nw ? w : 0) * P.rng_stride;   // over the ORCA scratch, dead after phase 2
         WRng m;
-        m.w = (uint32_t *)wb; m.lane = lane; m.phx = PHX;
+        m.w = (uint32_t *)wb; m.off = 0; m.lane = lane; m.phx = PHX; m.edbg = -1;
+        m.grid = P.rng_stride > CN_PEND_LDS ? wb + CN_PEND_LDS : nullptr;
         m.sl = (double *)(wb + 2 * CN_MT_N * 4 + 7 * 32 * 8);
         double *hb = (double *)(wb + 2 * CN_MT_N * 4);
         ResetOut o;
@@ -2212,8 +2449,8 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             if (need & 1u) {
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
-                const bool may = !g.pend.all && !(sl.rflag[EPB + q] & 8u);
-                reset_env(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, m, en);
+                const bool may = !g.pend.all;   // both pending slots are ready unless this launch draws all
+                reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, m, en);
                 if (lane == 0) g.plist_w[atomicAdd(g.pcount_w, 1u)] = (uint32_t)e;
                 STAMP_B(e, 5);
             } else {
@@ -2224,6 +2461,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 en.rgx = RF(sl, R_GX, q, EPB); en.rgy = RF(sl, R_GY, q, EPB); en.rr = RF(sl, R_RAD, q, EPB);
                 // update_human_goal checks every human AFTER the random changes (a new random goal may
                 // land within reach of its own human), so it runs whenever end goal changing is on
+                m.edbg = e;
                 goal_changes(c, S, e, en, m, (need & 2u) != 0, c.end_goal_changing != 0, hb);
             }
         }
@@ -2241,14 +2479,16 @@ __global__ void __launch_bounds__(64) cn_reset_kernel(RngArgs g, cn_config c)
     __shared__ uint32_t mtw[2 * CN_MT_N];
     __shared__ double hbuf[7][32];
     __shared__ double slots[6 * 64];
+    __shared__ __attribute__((aligned(16))) char gridbuf[CN_GRID_LDS];
     const int lane = threadIdx.x;
     for (int64_t e = blockIdx.x; e < g.E; e += gridDim.x) {
         Env1 en;
         en.hpx = hbuf[0]; en.hpy = hbuf[1]; en.hgx = hbuf[2]; en.hgy = hbuf[3]; en.hr = hbuf[4]; en.hvp = hbuf[5];
         en.hth = hbuf[6];
         WRng m;
-        m.w = mtw; m.lane = lane; m.sl = slots; m.phx = c.rng_mode == CN_RNG_PHILOX;
-        reset_env(g.o, g.pend, c, g.E, e, g.counter_offset, true, m, en);
+        m.w = mtw; m.off = 0; m.lane = lane; m.sl = slots; m.phx = c.rng_mode == CN_RNG_PHILOX; m.edbg = -1;
+        m.grid = gridbuf;
+        reset_env<true>(g.o, g.pend, c, g.E, e, g.counter_offset, true, m, en);
     }
 }
 
@@ -2631,8 +2871,9 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     if (g->case_size <= 0) { delete g; return set_err(CN_EINVAL, "case size (val_size/test_size) must be > 0"); }
     const int64_t E = g->E, EN = (int64_t)g->E * g->N;
     auto al = [](int64_t b) { return (b + 255) & ~(int64_t)255; };
-    const int64_t pb_mt = al(E * CN_MT_N * 4), pb_i = al(E * 4), pb_cc = al(E * 8), pb_r = al(5 * E * 8),
-                  pb_h = al(7 * EN * 8);
+    // pending spawns: every array holds both slots ([2][...], pend_slot)
+    const int64_t pb_mt = al(2 * E * CN_MT_N * 4), pb_i = al(2 * E * 4), pb_cc = al(2 * E * 8), pb_r = al(2 * 5 * E * 8),
+                  pb_h = al(2 * 7 * EN * 8);
     const int64_t pend_bytes = pb_mt + 5 * pb_i + pb_cc + pb_r + pb_h;
     hipError_t e1 = hipMalloc(&g->state, g->state_bytes);
     hipError_t e2 = hipMalloc(&g->work, sizeof(uint32_t) * (g->E + 64));
@@ -2666,7 +2907,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         // the plan holds phase 5's RNG regions (laid over the ORCA scratch); spare workgroups run as many
         // spawning waves as regions fit in the same allocation
         g->a_lds = g->plan.total;
-        const int fit = g->a_lds / CN_PEND_LDS;
+        const int fit = g->a_lds / g->plan.rng_stride;
         g->pend_waves = fit < g->plan.T / 64 ? fit : g->plan.T / 64;
         const int nw = g->pend_waves;
         const int64_t need = (E + nw - 1) / nw;
@@ -2785,6 +3026,8 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.pend.all = g->pend_all;
     a.pend.step_blocks = blocks; a.pend.pend_blocks = g->pend_blocks; a.pend.counter_offset = g->counter_offset;
     a.pend.waves = g->pend_waves;
+    a.pend.stride = g->plan.rng_stride;
+    a.pend.case_size = g->case_size;
     g->pend_all = 0;
     const int grid = blocks + g->pend_blocks;
     const bool phx = g->c.rng_mode == CN_RNG_PHILOX;
@@ -2838,6 +3081,13 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
 }
 
 #ifdef CN_STAMPS
+int cn_debug_stamps_c(unsigned long long *c)
+{
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(c, HIP_SYMBOL(cn_stamp_c), sizeof(unsigned long long) * 8192 * 4));
+    return CN_OK;
+}
+
 int cn_debug_stamps(unsigned long long *a, unsigned long long *b)
 {
     HIPCHK(hipDeviceSynchronize());

@@ -118,6 +118,15 @@ def run(variant, E=4096, N=10, steps=300):
                     print("        %d rounds: %4d envs, cycles median %d max %d | walk %d first-tries %d reject-loop %d (mean)" % (
                         r, sel.sum(), np.median(part[sel]), part[sel].max(), goal[sel, k0].mean(), goal[sel, k0 + 1].mean(),
                         goal[sel, k0 + 2].mean()))
+    if variant == "c3":
+        L.cn_debug_stamps_c.argtypes = [ctypes.c_void_p]
+        cc = np.zeros(8192 * 4, np.uint64)
+        L.cn_debug_stamps_c(cc.ctypes.data_as(ctypes.c_void_p))
+        C = cc.reshape(-1, 4).astype(np.float64)[:E]
+        n = C[:, 3].sum()
+        if n:
+            print("  crowded rejection, all steps: %d passes; per pass cycles: ensure (MT gen) %.0f, candidates %.0f, "
+                  "tests + ballot %.0f" % (n, C[:, 0].sum() / n, C[:, 1].sum() / n, C[:, 2].sum() / n))
     eng.close()
 
 
