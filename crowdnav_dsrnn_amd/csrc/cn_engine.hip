@@ -43,6 +43,7 @@ __device__ __forceinline__ void wsync()
 __device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_c[8192 * 4];   // crowded rejection: ensure / cand / test / passes
+__device__ unsigned long long cn_stamp_p[8192 * 2];   // spawn waves: start / end of each env's latest spawn
 #define STAMP_A(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + (k)] = clock64(); } while (0)
 #define STAMP_B(w, k) do { if ((threadIdx.x & 63) == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
 #else
@@ -1627,10 +1628,16 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         double rth;
         uint32_t ovf;
         int sc;
+#ifdef CN_STAMPS
+        const unsigned long long ts0 = clock64();
+#endif
         spawn_env<GRID>(c, c.env_offset + e, cc, rc, pl.counter_offset, m, en, rth, ovf, sc);
         const bool in1 = !m.phx && m.p > CN_MT_N;
         write_pending(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
                       lane);
+#ifdef CN_STAMPS
+        if (lane == 0 && e < 8192) { cn_stamp_p[2 * e] = ts0; cn_stamp_p[2 * e + 1] = clock64(); }
+#endif
         wsync();
     }
 }
@@ -3081,10 +3088,11 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
 }
 
 #ifdef CN_STAMPS
-int cn_debug_stamps_c(unsigned long long *c)
+int cn_debug_stamps_c(unsigned long long *c, unsigned long long *p)
 {
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpyFromSymbol(c, HIP_SYMBOL(cn_stamp_c), sizeof(unsigned long long) * 8192 * 4));
+    HIPCHK(hipMemcpyFromSymbol(p, HIP_SYMBOL(cn_stamp_p), sizeof(unsigned long long) * 8192 * 2));
     return CN_OK;
 }
 

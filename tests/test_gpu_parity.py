@@ -190,19 +190,31 @@ def test_gpu_vs_oracle_teacher_forced(gpu, oracle, kin, N, policy, scen, fov):
     assert mism == 0, mism
 
 
-@pytest.mark.parametrize("rng", ["mt19937", "philox"])
-def test_gpu_free_running_matches_oracle_short_horizon(gpu, oracle, rng):
-    """Free-running (no teacher forcing) C2-shaped rollout: identical for the first 40 steps (auto-resets
-    from the spawns the spare workgroups draw ahead included)."""
-    cfg = _cfg(10, "unicycle", E=512, env__rng=rng)
+@pytest.mark.parametrize("rng,shape", [("mt19937", "c2"), ("philox", "c2"), ("mt19937", "c3")])
+def test_gpu_free_running_matches_oracle_short_horizon(gpu, oracle, rng, shape):
+    """Free-running (no teacher forcing) rollout: identical for the first 40 steps, auto-resets from the
+    spawns the spare workgroups draw ahead included. c3 (25 humans, square_crossing, FOV pi, kd-tree path)
+    also runs the spawns' binned disc test and the workgroup-cooperative crowded rejection of the spare
+    workgroups (a few resets per step; teacher-forced tests redraw every spawn after set_state instead)."""
+    if shape == "c3":
+        cfg = _cfg(25, "holonomic", "square_crossing", E=512, fov=1.0, env__rng=rng)
+    else:
+        cfg = _cfg(10, "unicycle", E=512, env__rng=rng)
     ref, g = oracle.RefEngine(cfg), gpu(cfg)
     o1, o2 = ref.reset(), g.reset()
     for k in o1:
         np.testing.assert_allclose(o2[k], o1[k], atol=1e-6, rtol=0)
     rng = np.random.RandomState(11)
     for t in range(40):
-        a = rng.uniform(-0.1, 0.1, (cfg.num_envs, 2)).astype(np.float32)
+        a = (rng.uniform(-0.1, 0.1, (cfg.num_envs, 2)) if shape == "c2"
+             else rng.normal(0, 0.5, (cfg.num_envs, 2))).astype(np.float32)
         r1, r2 = ref.step(a), g.step(a)
         np.testing.assert_array_equal(r2[2], r1[2])
         np.testing.assert_array_equal(r2[3], r1[3])
         np.testing.assert_allclose(r2[1], r1[1], atol=1e-5, rtol=0)
+    if shape == "c3":   # every stream (spawn draws included) at the same position, states within 1e-5
+        rs, gs = ref.get_state(), g.get_state()
+        d = {"post_" + n: np.asarray(getattr(rs, n)) for n, _, _ in abi.STATE_FIELDS if n != "mt"}
+        d["post_mt_crc"] = H.mt_crc(rs)
+        errs = H.compare_state(gs, d, "post_", tol=1e-5)
+        assert not errs, errs

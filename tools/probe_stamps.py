@@ -119,9 +119,16 @@ def run(variant, E=4096, N=10, steps=300):
                         r, sel.sum(), np.median(part[sel]), part[sel].max(), goal[sel, k0].mean(), goal[sel, k0 + 1].mean(),
                         goal[sel, k0 + 2].mean()))
     if variant == "c3":
-        L.cn_debug_stamps_c.argtypes = [ctypes.c_void_p]
+        L.cn_debug_stamps_c.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         cc = np.zeros(8192 * 4, np.uint64)
-        L.cn_debug_stamps_c(cc.ctypes.data_as(ctypes.c_void_p))
+        pp = np.zeros(8192 * 2, np.uint64)
+        L.cn_debug_stamps_c(cc.ctypes.data_as(ctypes.c_void_p), pp.ctypes.data_as(ctypes.c_void_p))
+        P = pp.reshape(-1, 2).astype(np.int64)[:E]
+        ok = P[:, 1] > P[:, 0]
+        if ok.any():
+            dur = P[ok, 1] - P[ok, 0]    # the latest spawn of each env (s_memtime differs across XCDs: durations only)
+            print("  spawn waves (latest spawn per env, %d envs): cycles median %d p90 %d max %d" % (
+                ok.sum(), np.median(dur), np.percentile(dur, 90), dur.max()))
         C = cc.reshape(-1, 4).astype(np.float64)[:E]
         n = C[:, 3].sum()
         if n:
