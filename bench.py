@@ -34,8 +34,9 @@ WORKLOAD_DESC = {
           "holonomic robot, actions N(0,0.5^2), auto-reset",
     "c4": "C4: %d envs/GPU x %d humans, circle_crossing, ORCA humans, holonomic robot, DSRNN act() in the loop "
           "(sampled actions), PPO num_steps=128 epochs=5 minibatches=2, grads all-reduced over RCCL",
-    "c5": "C5: %d envs/GPU (%s humans: traffic / side-preference halves), per-env scenario dispatch over "
-          "parallel/perpendicular traffic and the 3 side_pref scenarios, norm-zone reward, holonomic",
+    "c5": "C5: %d envs/GPU in ONE mixed engine, per-env scenario dispatch round-robin over parallel / "
+          "perpendicular traffic (%s humans) and the 3 side_pref scenarios (1 human, padded), norm-zone reward, "
+          "holonomic, ORCA",
 }
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 
@@ -48,8 +49,7 @@ def algorithmic_bytes_per_env_step(N):
 
 def make_config(E, N, env_offset, nenv, workload="c2", rng="mt19937"):
     """SURVEY.md §8d workloads. c2 (default, the BASELINE metric): circle_crossing, ORCA, unicycle.
-    c3: square_crossing ("random crossing"), robot/human FOV = pi, holonomic. c5 is two engines
-    (see engines_for)."""
+    c3: square_crossing ("random crossing"), robot/human FOV = pi, holonomic. c5: c5_mixed."""
     from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config
 
     c = clone_config(Config())
@@ -65,21 +65,20 @@ def make_config(E, N, env_offset, nenv, workload="c2", rng="mt19937"):
     return make_cn_config(c, num_envs=E, env_offset=env_offset, nenv=nenv, phase="train", rng=rng)
 
 
-def engines_for(workload, E, N, rank, world, rng="mt19937"):
-    """(list of cn_config, per-engine action kind) for one rank. C5: per-env scenario
-    dispatch round-robin over {parallel, perpendicular} traffic (N = 5) and the three side-preference
-    scenarios (N = 1, circle radius 4, fixed robot), norm-zone reward and social metrics on: one engine
-    per human count, half of the envs each."""
-    from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config
+C5_SCENARIOS = ["parallel_traffic", "perpendicular_traffic", "side_pref_passing", "side_pref_overtaking",
+                "side_pref_crossing"]
 
-    if workload != "c5":
-        return [(make_config(E, N, rank * E, E * world, workload, rng), workload)]
-    out = []
-    half = E // 2
-    for k, (scen, n) in enumerate(((["parallel_traffic", "perpendicular_traffic"], 5),
-                                   (["side_pref_passing", "side_pref_overtaking", "side_pref_crossing"], 1))):
+
+def c5_scenario_configs():
+    """{scenario: reference-style config}. Traffic scenarios: N = 5; the side-preference
+    scenarios: N = 1, circle radius 4, fixed robot (0, -4) -> (0, 4), no goal changing (config.py:37-40,
+    95,99; crowd_sim.py:642-651). Norm-zone reward ("social-metric reward") everywhere,
+    holonomic robot, ORCA humans."""
+    from crowdnav_dsrnn_amd.config import Config, clone_config
+
+    out = {}
+    for scen, n in (("traffic", 5), ("side_pref", 1)):
         c = clone_config(Config())
-        c.sim.train_val_sim = c.sim.test_sim = scen
         c.sim.human_num = n
         c.humans.policy = "orca"
         c.action_space.kinematics = "holonomic"
@@ -89,9 +88,19 @@ def engines_for(workload, E, N, rank, world, rng="mt19937"):
             c.sim.circle_radius = 4
             c.humans.random_goal_changing = False
             c.humans.end_goal_changing = False
-        out.append((make_cn_config(c, num_envs=half, env_offset=rank * half, nenv=half * world, phase="train",
-                                   rng=rng), "c5"))
+        for s in C5_SCENARIOS:
+            if s.startswith("side_pref") == (scen == "side_pref"):
+                out[s] = c
     return out
+
+
+def c5_mixed(E, env_offset, nenv, rng="mt19937"):
+    """(group cn_configs, env_group) of the C5 mixed engine: env r runs C5_SCENARIOS[(env_offset + r) % 5]
+    (round-robin by global env index) with that scenario's human count."""
+    from crowdnav_dsrnn_amd.config import make_mixed_cn_configs
+
+    return make_mixed_cn_configs(c5_scenario_configs(), C5_SCENARIOS, E, env_offset=env_offset, nenv=nenv,
+                                 phase="train", rng=rng)
 
 
 def _oracle_rate(cfg, budget_s, threads, kind="uniform"):
@@ -311,7 +320,12 @@ def main():
         N = 25
     if args.workload == "c5" and E == 4096:
         E = 8192
-    engs = [CrowdNavEngine(cfg, device) for cfg, _ in engines_for(args.workload, E, N, rank, world, args.rng)]
+    if args.workload == "c5":
+        N = 5
+        cfgs, env_group = c5_mixed(E, rank * E, E * world, args.rng)
+        engs = [CrowdNavEngine.mixed(cfgs, env_group, device)]
+    else:
+        engs = [CrowdNavEngine(make_config(E, N, rank * E, E * world, args.workload, args.rng), device)]
     eng = engs[0]
     gen = torch.Generator(device=device)
     gen.manual_seed(rank)
@@ -355,8 +369,12 @@ def main():
     E_total = sum(e_.E for e_ in engs)
     if rank == 0:
         value = world * E_total * K / elapsed
-        kernel_s = a_ms.value / 1e3 / max(n.value, 1)
-        bpl = algorithmic_bytes_per_env_step(eng.N) * eng.E   # the timed kernel is engs[0]'s
+        kernel_s = a_ms.value / 1e3 / max(n.value, 1)   # c5: both group launches of a step
+        if args.workload == "c5":   # per group: its envs x B_step(its own N) (padding rows not counted)
+            hum = eng.env_humans.cpu().numpy()
+            bpl = int(sum(algorithmic_bytes_per_env_step(int(n)) for n in hum))
+        else:
+            bpl = algorithmic_bytes_per_env_step(eng.N) * eng.E
         achieved = bpl / kernel_s / 1e9
         pmc = load_pmc("cn_step_kernel", args.workload)
         line = {
@@ -374,7 +392,7 @@ def main():
             "data": "synthetic",
             "config": {
                 "workload": WORKLOAD_DESC[args.workload] % (E_total, N),
-                "envs_per_gpu": E_total, "humans": N if args.workload != "c5" else "5 / 1",
+                "envs_per_gpu": E_total, "humans": N if args.workload != "c5" else "5 (traffic) / 1 (side_pref)",
                 "global_envs": E_total * world,
                 "parallelism": "env-sharded x%d (no collective)" % world,
                 "rng": args.rng,

@@ -55,6 +55,8 @@ def lib():
     _check_provenance(L)
     L.cn_config_validate.argtypes = [cfgp]
     L.cn_create.argtypes = [cfgp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.cn_create_mixed.argtypes = [cfgp, ctypes.c_int, vp, i64, ctypes.c_int, ctypes.POINTER(vp)]
+    L.cn_env_humans.argtypes = [vp, vp]
     L.cn_destroy.argtypes = [vp]
     L.cn_destroy.restype = None
     L.cn_reset.argtypes = [vp, vp, vp, vp, vp]
@@ -80,7 +82,7 @@ def lib():
     L.cn_profile.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.cn_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(i64)]
-    for f in ("cn_config_validate", "cn_create", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
+    for f in ("cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
               "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features", "cn_profile",
               "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64"):
         getattr(L, f).restype = i32
@@ -94,7 +96,8 @@ def check(rc):
     return rc
 
 
-EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "cn_destroy", "cn_reset", "cn_step",
+EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans",
+            "cn_destroy", "cn_reset", "cn_step",
             "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
             "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter",
             "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad",

@@ -279,3 +279,27 @@ def clone_config(config):
         if type(val).__name__ == "BaseConfig":
             setattr(new, name, copy.deepcopy(val))
     return new
+
+
+def make_mixed_cn_configs(scenario_configs, scenarios, num_envs, env_offset=0, nenv=None, phase=None, rng=None):
+    """Per-env scenario dispatch with per-env human counts for CrowdNavEngine.mixed.
+
+    `scenarios` is the round-robin scenario list: env r (global index env_offset + r) runs
+    scenarios[(env_offset + r) % len(scenarios)] (the engine's deterministic stand-in for the reference's
+    per-reset `random.choices`, crowd_sim_dict.py:110-125). `scenario_configs` maps each scenario name to
+    the reference-style config its envs use (human_num, circle_radius, test.side_preference, goal
+    changing, ... -- e.g. the side_pref_* scenarios at N = 1, crowd_sim.py:334-357,642-651); scenarios
+    that share one config object share one group. Returns (list of cn_config, env_group int32 [num_envs])."""
+    nenv = num_envs if nenv is None else nenv
+    keys, groups, env_group = [], [], np.zeros(num_envs, np.int32)
+    for s in scenarios:
+        if id(scenario_configs[s]) not in keys:
+            keys.append(id(scenario_configs[s]))
+            groups.append(scenario_configs[s])
+    sc_group = [keys.index(id(scenario_configs[s])) for s in scenarios]
+    for r in range(num_envs):
+        env_group[r] = sc_group[(env_offset + r) % len(scenarios)]
+    cfgs = [make_cn_config(c, num_envs=int((env_group == g).sum()), env_offset=env_offset, nenv=nenv, phase=phase,
+                           scenarios=list(scenarios), scenario_mode=abi.SCMODE_ROUND_ROBIN, rng=rng)
+            for g, c in enumerate(groups)]
+    return cfgs, env_group

@@ -14,6 +14,7 @@
 // crowd_sim/envs/utils/agent.py:172-218, crowd_nav/policy/{orca,social_force,srnn}.py; RVO2 v2.0
 // (third-party) restated in float32. Numerics: see cn_math.h.
 #include <hip/hip_runtime.h>
+#include <vector>
 #include <math.h>
 #include <stdio.h>
 #include <string.h>
@@ -706,11 +707,25 @@ __host__ __device__ inline PendPtrs pend_slot(const PendPtrs &P, int s, int64_t 
     return q;
 }
 
+// Output view of a group engine inside a mixed engine (cn_create_mixed): local env e of
+// the group is row `row[e]` of the caller's (E_total, ...) buffers, whose spatial_edges have NS human
+// slots (NS >= N; slots N..NS-1 are padding). row == nullptr: identity, NS == N (a plain engine).
+struct OutView {
+    const int32_t *row;
+    int NS;
+};
+__device__ __forceinline__ int64_t orow(const OutView &v, int64_t e) { return v.row ? (int64_t)v.row[e] : e; }
+// padding slot of a mixed engine's spatial_edges: a human that is never seen, i.e. the belief the
+// reference gives an unseen human at reset (crowd_sim.py:437-455: [15, 15, 0, 0, 0.3], zero velocity, so
+// it never moves), relative to the robot
+#define CN_PAD_POS 15.0
+
 // where a reset writes: state + the first observation of the new episode
 struct ResetOut {
     cn_state_ptrs s;
     float *robot_node, *temporal, *spatial;
     int64_t case_size;
+    OutView ov;
 };
 
 struct RngArgs {   // cn_reset_kernel
@@ -1297,6 +1312,11 @@ __device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &
     const int N = c.human_num;
     const int64_t hb = e * N;
     const double rpx = en.rpx, rpy = en.rpy;
+    const int64_t orw = orow(g.ov, e);
+    if (lane >= N && lane < g.ov.NS) {
+        g.spatial[(orw * g.ov.NS + lane) * 2] = (float)(CN_PAD_POS - rpx);
+        g.spatial[(orw * g.ov.NS + lane) * 2 + 1] = (float)(CN_PAD_POS - rpy);
+    }
     if (lane < N) {
         const int64_t h = hb + lane;
         const double px = en.hpx[lane], py = en.hpy[lane];
@@ -1312,8 +1332,8 @@ __device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &
         if (v) { bpx = px; bpy = py; bvx = 0; bvy = 0; br = en.hr[lane]; }
         else { bpx = 15.0; bpy = 15.0; bvx = 0.0; bvy = 0.0; br = 0.3; }
         S.b_px[h] = bpx; S.b_py[h] = bpy; S.b_vx[h] = bvx; S.b_vy[h] = bvy; S.b_r[h] = br;
-        g.spatial[h * 2] = (float)(bpx - rpx);
-        g.spatial[h * 2 + 1] = (float)(bpy - rpy);
+        g.spatial[(orw * g.ov.NS + lane) * 2] = (float)(bpx - rpx);
+        g.spatial[(orw * g.ov.NS + lane) * 2 + 1] = (float)(bpy - rpy);
     }
     const int A = N + (c.robot_visible ? 1 : 0);
     if (A > 10) for (int k = lane; k < N * A; k += 64) S.o_perm[e * N * A + k] = 0;
@@ -1335,10 +1355,10 @@ __device__ __forceinline__ void write_reset(const ResetOut &g, const cn_config &
         S.reset_count[e] += 1;
         S.ep_return[e] = 0.0; S.ep_len[e] = 0;
         S.flags[e] = 0; S.overflow[e] = ovf; S.mt_pos[e] = pos;
-        float *rn = g.robot_node + e * 7;
+        float *rn = g.robot_node + orw * 7;
         rn[0] = (float)rpx; rn[1] = (float)rpy; rn[2] = (float)c.robot_radius;
         rn[3] = (float)en.rgx; rn[4] = (float)en.rgy; rn[5] = (float)c.robot_vpref; rn[6] = (float)rth;
-        g.temporal[e * 2] = 0.0f; g.temporal[e * 2 + 1] = 0.0f;
+        g.temporal[orw * 2] = 0.0f; g.temporal[orw * 2 + 1] = 0.0f;
     }
 }
 
@@ -1579,7 +1599,7 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2,
         double rth;
         uint32_t ovf;
         int sc;
-        spawn_env<GRID>(c, c.env_offset + e, cc, rc, counter_offset, m, en, rth, ovf, sc);
+        spawn_env<GRID>(c, c.env_offset + orow(o.ov, e), cc, rc, counter_offset, m, en, rth, ovf, sc);
         const bool in1 = !m.phx && m.p > CN_MT_N;
         write_reset(o, c, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, lane);
     }
@@ -1598,6 +1618,7 @@ struct PendLaunch {
     int stride;             // bytes per spawning wave's region (StepPlan::rng_stride)
     int64_t counter_offset;
     int64_t case_size;
+    OutView ov;             // global env index = c.env_offset + orow(ov, e)
 };
 
 // GRID: the spawn's crowded rejection through a DiscGrid (the kd-tree path's plans have LDS for it)
@@ -1631,7 +1652,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
 #ifdef CN_STAMPS
         const unsigned long long ts0 = clock64();
 #endif
-        spawn_env<GRID>(c, c.env_offset + e, cc, rc, pl.counter_offset, m, en, rth, ovf, sc);
+        spawn_env<GRID>(c, c.env_offset + orow(pl.ov, e), cc, rc, pl.counter_offset, m, en, rth, ovf, sc);
         const bool in1 = !m.phx && m.p > CN_MT_N;
         write_pending(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
                       lane);
@@ -1661,6 +1682,7 @@ struct StepArgs {
     PendLaunch pend;        // spawn waves: workgroups [step_blocks, step_blocks + pend_blocks)
     int64_t case_size;
     int E;
+    OutView ov;             // output rows / human stride (mixed engines); also pend.ov
 };
 
 // observed agent of slot k seen by lane (human i of env base eb): position/velocity float32,
@@ -1778,7 +1800,8 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         rv[R_LAX] = S.last_ax[ge]; rv[R_LAY] = S.last_ay[ge]; rv[R_EPR] = S.ep_return[ge];
         const uint32_t fl = S.flags[ge];
         pre_epl = S.ep_len[ge]; pre_sc = S.scenario[ge]; pre_ovf = S.overflow[ge];
-        float a0 = g.actions[ge * 2], a1 = g.actions[ge * 2 + 1];
+        const int64_t oa = orow(g.ov, ge);   // the env's row in the caller's buffers
+        float a0 = g.actions[oa * 2], a1 = g.actions[oa * 2 + 1];
         asm volatile("" ::: "memory");
         RF(sl, R_PX, re, EPB) = rv[R_PX]; RF(sl, R_PY, re, EPB) = rv[R_PY];
         RF(sl, R_GX, re, EPB) = rv[R_GX]; RF(sl, R_GY, re, EPB) = rv[R_GY];
@@ -2320,7 +2343,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             else reward = (double)(((float)reward + r_spin) + r_back);
         }
         if (g.info) {
-            float *info = g.info + ge * CN_INFO_K;
+            float *info = g.info + orow(g.ov, ge) * CN_INFO_K;
             info[CN_INFO_AGG_NAV_TIME] = (float)agg;
             info[CN_INFO_PATH_VIOLATION] = (float)vr_viol;
             info[CN_INFO_PERSONAL_VIOLATION] = dmin < c.min_personal_space ? 1.0f : 0.0f;
@@ -2345,11 +2368,12 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const double epr = RF(sl, R_EPR, re, EPB) + reward;
         const int32_t epl = pre_epl + 1;
         S.ep_return[ge] = epr; S.ep_len[ge] = epl;
-        if (g.reward) g.reward[ge] = (float)reward;
-        if (g.done) g.done[ge] = (uint8_t)done;
-        if (g.event) g.event[ge] = (int8_t)event;
-        if (g.ep_return) g.ep_return[ge] = epr;
-        if (g.ep_len) g.ep_len[ge] = epl;
+        const int64_t oe = orow(g.ov, ge);
+        if (g.reward) g.reward[oe] = (float)reward;
+        if (g.done) g.done[oe] = (uint8_t)done;
+        if (g.event) g.event[oe] = (int8_t)event;
+        if (g.ep_return) g.ep_return[oe] = epr;
+        if (g.ep_len) g.ep_len[oe] = epl;
         sl.rflag[EPB + re] = (uint32_t)done;   // aux word: done
     }
     __syncthreads();
@@ -2378,8 +2402,9 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             bpx = HF(sl, H_BPX, tid) + bvx * dt; bpy = HF(sl, H_BPY, tid) + bvy * dt;
         }
         S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = bvx; S.b_vy[gh] = bvy; S.b_r[gh] = br;
-        g.spatial[gh * 2] = (float)(bpx - rnx);
-        g.spatial[gh * 2 + 1] = (float)(bpy - rny);
+        const int64_t oh = orow(g.ov, e0 + el) * g.ov.NS + i;
+        g.spatial[oh * 2] = (float)(bpx - rnx);
+        g.spatial[oh * 2 + 1] = (float)(bpy - rny);
         uint32_t f = sl.lf[tid] & ~LF_ENDGOAL;
         if (np_norm2(HF(sl, H_GX, tid) - npx, HF(sl, H_GY, tid) - npy) < HF(sl, H_R, tid)) f |= LF_ENDGOAL;
         if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
@@ -2406,12 +2431,17 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         }
         if (nan) flags |= CN_FLAG_NAN;
         S.flags[ge] = flags;
-        float *rn = g.robot_node + ge * 7;
+        const int64_t oe = orow(g.ov, ge);
+        float *rn = g.robot_node + oe * 7;
         rn[0] = (float)nx; rn[1] = (float)ny; rn[2] = (float)RF(sl, R_RAD, re, EPB);
         rn[3] = (float)RF(sl, R_GX, re, EPB); rn[4] = (float)RF(sl, R_GY, re, EPB);
         rn[5] = (float)RF(sl, R_VP, re, EPB); rn[6] = (float)RF(sl, R_TH, re, EPB);
-        g.temporal[ge * 2] = (float)RF(sl, R_VX, re, EPB);
-        g.temporal[ge * 2 + 1] = (float)RF(sl, R_VY, re, EPB);
+        g.temporal[oe * 2] = (float)RF(sl, R_VX, re, EPB);
+        g.temporal[oe * 2 + 1] = (float)RF(sl, R_VY, re, EPB);
+        for (int k = N; k < g.ov.NS; ++k) {   // padding slots of a mixed engine (never-seen humans)
+            g.spatial[(oe * g.ov.NS + k) * 2] = (float)(CN_PAD_POS - nx);
+            g.spatial[(oe * g.ov.NS + k) * 2 + 1] = (float)(CN_PAD_POS - ny);
+        }
         // random numbers needed? (crowd_sim_dict.py:260-269, shmem_vec_env.py:166-167)
         const bool done = sl.rflag[EPB + re] != 0;
         const bool rgoal = c.random_goal_changing && np_mod(gt, 5.0) == 0.0;
@@ -2436,6 +2466,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         double *hb = (double *)(wb + 2 * CN_MT_N * 4);
         ResetOut o;
         o.s = S; o.robot_node = g.robot_node; o.temporal = g.temporal; o.spatial = g.spatial; o.case_size = g.case_size;
+        o.ov = g.ov;
         // waves without an env to serve skip the block entirely: the loop's preheader (values the
         // compiler hoists out of the RNG work, and their spill stores) then runs only where it is needed
         bool mine = false;
@@ -2726,6 +2757,14 @@ struct cn_engine {
     // kernel timing (cn_profile)
     int prof_on, prof_cap, prof_n;
     hipEvent_t *ev;  // [2]: before the first, after the last launch of the window
+    // output view (a group of a mixed engine: its envs' rows in the caller's buffers and the padded human
+    // stride; identity / N for a plain engine)
+    int32_t *rows;   // device [E] or nullptr
+    int NS;
+    // mixed engine (cn_create_mixed): the groups, each a plain engine over its envs; E = all envs,
+    // N = NS = the largest human count
+    int ngroups;
+    cn_engine **grp;
 };
 
 static thread_local char g_err[512];
@@ -2789,6 +2828,35 @@ __global__ void __launch_bounds__(64) cn_orca_kernel(int64_t n, int A, const flo
             out[4 * i] = rx; out[4 * i + 1] = ry; out[4 * i + 2] = (float)fail_at; out[4 * i + 3] = (float)cnt;
         }
     }
+}
+
+// cn_social_force_predict: SOCIAL_FORCE.predict (social_force.py:11-66) for n agents, one lane each, f64 in
+// the reference's operation order (the step kernel's phase 2 on caller-given states)
+__global__ void __launch_bounds__(64) cn_sf_predict_kernel(int64_t n, int M, const double *__restrict__ self,
+                                                           const double *__restrict__ others, double A, double B,
+                                                           double KI, double dt, double *__restrict__ out)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double *s = self + 9 * i;   // px, py, vx, vy, radius, gx, gy, v_pref, theta
+    const double px = s[0], py = s[1], vx0 = s[2], vy0 = s[3], rad = s[4], vpref = s[7];
+    const double gdx = s[5] - px, gdy = s[6] - py;
+    const double dg = dsqrt(gdx * gdx + gdy * gdy);
+    const double dvx = ddiv(gdx, dg) * vpref, dvy = ddiv(gdy, dg) * vpref;
+    const double cdx = KI * (dvx - vx0), cdy = KI * (dvy - vy0);
+    double ix = 0.0, iy = 0.0;
+    for (int k = 0; k < M; ++k) {
+        const double *o = others + (i * M + k) * 5;   // px, py, vx, vy, radius
+        const double ddx = px - o[0], ddy = py - o[1];
+        const double d = dsqrt(ddx * ddx + ddy * ddy);
+        const double ex = exp(ddiv(rad + o[4] - d, B));
+        ix += A * ex * ddiv(ddx, d);
+        iy += A * ex * ddiv(ddy, d);
+    }
+    const double nx = vx0 + (cdx + ix) * dt, ny = vy0 + (cdy + iy) * dt;
+    const double nn = np_norm2(nx, ny);
+    if (nn > vpref) { out[2 * i] = ddiv(nx, nn) * vpref; out[2 * i + 1] = ddiv(ny, nn) * vpref; }
+    else { out[2 * i] = nx; out[2 * i + 1] = ny; }
 }
 
 extern "C" {
@@ -2867,6 +2935,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     g->device = device;
     g->E = cfg->num_envs;
     g->N = cfg->human_num;
+    g->NS = g->N;
     g->A = cn_sim_agents(g->N, cfg->robot_visible);
     g->plan = cn_step_plan(g->N, cfg->robot_visible);
     g->state_bytes = cn_state_layout(g->E, g->N, cfg->robot_visible, nullptr);
@@ -2942,6 +3011,84 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     return CN_OK;
 }
 
+// Mixed engine (per-env scenario dispatch with per-env human counts). Env r of the engine
+// (global index cfg.env_offset + r) belongs to group env_group[r]; each group is a plain engine over its
+// envs with its own cn_config (human count, scenario set, circle radius, side preference, goal changing,
+// ...), stepping them in the caller's (E, ...) buffers at their own rows (spatial_edges padded to the
+// largest human count). Seeds and round-robin scenarios use the global index, so groups[g].scenarios
+// must be the full scenario list and env r's scenario (scenarios[(env_offset + r) % num_scenarios]) must
+// be one its group was configured for -- which the caller guarantees by assigning groups per scenario.
+int cn_create_mixed(const cn_config *groups, int num_groups, const int32_t *env_group, int64_t num_envs, int device,
+                    cn_engine **out)
+{
+    if (!out) return set_err(CN_EINVAL, "null out");
+    *out = nullptr;
+    if (!groups || !env_group || num_groups < 1 || num_groups > 64 || num_envs <= 0)
+        return set_err(CN_EINVAL, "cn_create_mixed: 1..64 groups, env_group[num_envs] required");
+    if (num_envs >= (1LL << 31) / 64) return set_err(CN_EUNSUPPORTED, "cn_create_mixed: too many envs");
+    std::vector<std::vector<int32_t>> rows(num_groups);
+    for (int64_t r = 0; r < num_envs; ++r) {
+        if (env_group[r] < 0 || env_group[r] >= num_groups) return set_err(CN_EINVAL, "cn_create_mixed: env_group out of range");
+        rows[env_group[r]].push_back((int32_t)r);
+    }
+    int NS = 0;
+    for (int k = 0; k < num_groups; ++k) {
+        const cn_config &c = groups[k];
+        if ((int64_t)c.num_envs != (int64_t)rows[k].size())
+            return set_err(CN_EINVAL, "cn_create_mixed: groups[g].num_envs must equal the envs assigned to group g");
+        if (c.env_offset != groups[0].env_offset || c.nenv != groups[0].nenv || c.seed != groups[0].seed ||
+            c.phase != groups[0].phase)
+            return set_err(CN_EINVAL, "cn_create_mixed: env_offset / nenv / seed / phase must agree across groups");
+        if (c.scenario_mode != CN_SCMODE_ROUND_ROBIN)
+            return set_err(CN_EUNSUPPORTED, "cn_create_mixed: round-robin scenario mode only");
+        NS = c.human_num > NS ? c.human_num : NS;
+    }
+    HIPCHK(hipSetDevice(device));
+    cn_engine *m = new cn_engine();
+    m->c = groups[0];
+    m->c.num_envs = (int32_t)num_envs;
+    m->c.human_num = NS;
+    m->device = device;
+    m->E = (int)num_envs;
+    m->N = m->NS = NS;
+    m->grp = new cn_engine *[num_groups]();
+    for (int k = 0; k < num_groups; ++k) {
+        if (groups[k].num_envs == 0) continue;
+        int rc = cn_create(&groups[k], device, &m->grp[m->ngroups]);
+        if (rc) { cn_destroy(m); return rc; }
+        cn_engine *g = m->grp[m->ngroups++];
+        g->NS = NS;
+        if (hipMalloc(&g->rows, sizeof(int32_t) * rows[k].size()) != hipSuccess) {
+            cn_destroy(m);
+            return set_err(CN_ENOMEM, "hipMalloc failed");
+        }
+        if (hipMemcpy(g->rows, rows[k].data(), sizeof(int32_t) * rows[k].size(), hipMemcpyHostToDevice) != hipSuccess) {
+            cn_destroy(m);
+            return set_err(CN_EHIP, "hipMemcpy failed");
+        }
+        m->state_bytes += g->state_bytes;
+    }
+    *out = m;
+    return CN_OK;
+}
+
+// per-env human count of an engine (plain: N everywhere), into host memory [E]
+int cn_env_humans(const cn_engine *g, int32_t *dst)
+{
+    if (!g || !dst) return set_err(CN_EINVAL, "null argument");
+    if (!g->ngroups) {
+        for (int64_t r = 0; r < g->E; ++r) dst[r] = g->N;
+        return CN_OK;
+    }
+    for (int k = 0; k < g->ngroups; ++k) {
+        const cn_engine *q = g->grp[k];
+        std::vector<int32_t> rows(q->E);
+        HIPCHK(hipMemcpy(rows.data(), q->rows, sizeof(int32_t) * q->E, hipMemcpyDeviceToHost));
+        for (int64_t e = 0; e < q->E; ++e) dst[rows[e]] = q->N;
+    }
+    return CN_OK;
+}
+
 static void prof_free(cn_engine *g)
 {
     if (g->ev) {
@@ -2988,6 +3135,13 @@ void cn_destroy(cn_engine *g)
     if (!g) return;
     (void)hipSetDevice(g->device);
     prof_free(g);
+    if (g->ngroups) {
+        for (int k = 0; k < g->ngroups; ++k) cn_destroy(g->grp[k]);
+        delete[] g->grp;
+        delete g;
+        return;
+    }
+    (void)hipFree(g->rows);
     (void)hipFree(g->state);
     (void)hipFree(g->work);
     (void)hipFree(g->work_count);
@@ -3000,9 +3154,17 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
 {
     if (!g || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
+    if (g->ngroups) {
+        for (int k = 0; k < g->ngroups; ++k) {
+            const int rc = cn_reset(g->grp[k], stream, robot_node, temporal, spatial);
+            if (rc) return rc;
+        }
+        return CN_OK;
+    }
     RngArgs a;
     a.o.s = g->s; a.o.robot_node = robot_node; a.o.temporal = temporal; a.o.spatial = spatial;
     a.o.case_size = g->case_size;
+    a.o.ov.row = g->rows; a.o.ov.NS = g->NS;
     a.pend = g->pend; a.E = g->E; a.counter_offset = g->counter_offset;
     hipLaunchKernelGGL(cn_reset_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
     HIPCHK(hipGetLastError());
@@ -3020,6 +3182,15 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     ++g->nstep;
     const bool prof = g->prof_on && g->prof_n < g->prof_cap;
     if (prof && g->prof_n == 0) HIPCHK(hipEventRecord(g->ev[0], st));
+    if (g->ngroups) {   // one step launch per group, back to back on the stream
+        for (int k = 0; k < g->ngroups; ++k) {
+            const int rc = cn_step(g->grp[k], stream, actions, robot_node, temporal, spatial, reward, done, event, info,
+                                   ep_return, ep_len);
+            if (rc) return rc;
+        }
+        if (prof && ++g->prof_n == g->prof_cap) HIPCHK(hipEventRecord(g->ev[1], st));
+        return CN_OK;
+    }
     StepArgs a;
     a.s = g->s; a.actions = actions; a.robot_node = robot_node; a.temporal = temporal; a.spatial = spatial;
     a.reward = reward; a.done = done; a.event = event; a.info = info; a.ep_return = ep_return; a.ep_len = ep_len;
@@ -3035,6 +3206,8 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.pend.waves = g->pend_waves;
     a.pend.stride = g->plan.rng_stride;
     a.pend.case_size = g->case_size;
+    a.ov.row = g->rows; a.ov.NS = g->NS;
+    a.pend.ov = a.ov;
     g->pend_all = 0;
     const int grid = blocks + g->pend_blocks;
     const bool phx = g->c.rng_mode == CN_RNG_PHILOX;
@@ -3058,12 +3231,21 @@ int cn_state_bytes(const cn_engine *g, int64_t *bytes)
     return CN_OK;
 }
 
-const void *cn_state_device_ptr(const cn_engine *g) { return g ? g->state : nullptr; }
+const void *cn_state_device_ptr(const cn_engine *g) { return g && !g->ngroups ? g->state : nullptr; }
 
 int cn_get_state(cn_engine *g, void *stream, void *dst, int dst_on_host)
 {
     if (!g || !dst) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
+    if (g->ngroups) {   // the groups' blobs, concatenated in group order
+        char *d = (char *)dst;
+        for (int k = 0; k < g->ngroups; ++k) {
+            const int rc = cn_get_state(g->grp[k], stream, d, dst_on_host);
+            if (rc) return rc;
+            d += g->grp[k]->state_bytes;
+        }
+        return CN_OK;
+    }
     if (dst_on_host) {
         HIPCHK(hipMemcpyAsync(dst, g->state, g->state_bytes, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -3077,6 +3259,15 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
 {
     if (!g || !src) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
+    if (g->ngroups) {
+        const char *d = (const char *)src;
+        for (int k = 0; k < g->ngroups; ++k) {
+            const int rc = cn_set_state(g->grp[k], stream, d, src_on_host);
+            if (rc) return rc;
+            d += g->grp[k]->state_bytes;
+        }
+        return CN_OK;
+    }
     if (src_on_host) {
         HIPCHK(hipMemcpyAsync(g->state, src, g->state_bytes, hipMemcpyHostToDevice, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -3109,6 +3300,7 @@ int cn_lidar_obs(cn_engine *g, void *stream, const uint8_t *reset_mask, int enab
                  double robot_radius, float *lidar, float *obs)
 {
     if (!g) return set_err(CN_EINVAL, "null engine");
+    if (g->ngroups) return set_err(CN_EUNSUPPORTED, "cn_lidar_obs: not on a mixed engine");
     if (beams < 2 || beams > 4096 || !(max_range > 0) || !lidar || !obs)
         return set_err(CN_EINVAL, "cn_lidar_obs: beams in [2, 4096], max_range > 0 and buffers required");
     hipLaunchKernelGGL(cn_lidar_obs_kernel, dim3((unsigned)((g->E + 3) / 4)), dim3(256), 0, (hipStream_t)stream, g->s,
@@ -3144,6 +3336,23 @@ int cn_debug_orca(void *stream, int64_t n, int A, const float *agents, const flo
     if (A < 1 || A > 10) return set_err(CN_EUNSUPPORTED, "cn_debug_orca: 1 <= A <= 10 (the quad path)");
     hipLaunchKernelGGL(cn_orca_kernel, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, (hipStream_t)stream, n, A,
                        agents, self, neighbor_dist, time_horizon, time_step, out);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
+
+int cn_orca_predict(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
+                    float time_horizon, float time_step, float *out)
+{
+    return cn_debug_orca(stream, n, A, agents, self, neighbor_dist, time_horizon, time_step, out);
+}
+
+int cn_social_force_predict(void *stream, int64_t n, int M, const double *self, const double *others, double A,
+                            double B, double KI, double time_step, double *out)
+{
+    if (n <= 0 || M < 0 || M > 64 || !self || (M && !others) || !out)
+        return set_err(CN_EINVAL, "cn_social_force_predict: n > 0, 0 <= M <= 64 and buffers required");
+    hipLaunchKernelGGL(cn_sf_predict_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, n, M,
+                       self, others, A, B, KI, time_step, out);
     HIPCHK(hipGetLastError());
     return CN_OK;
 }

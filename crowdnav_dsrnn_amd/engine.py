@@ -20,25 +20,45 @@ class CrowdNavEngine:
     Returned tensors are the engine's own buffers (overwritten by the next call); clone to keep them.
     """
 
-    def __init__(self, cfg, device=None):
+    def __init__(self, cfg, device=None, _mixed=None):
         import torch
 
         self.torch = torch
         if not torch.cuda.is_available():
             raise RuntimeError("CrowdNavEngine needs a ROCm GPU (torch.cuda.is_available() is False)")
-        self.cfg = cfg.copy()
-        self.E, self.N = int(cfg.num_envs), int(cfg.human_num)
         self.device = torch.device(device if device is not None else "cuda:%d" % torch.cuda.current_device())
         L = _lib.lib()
-        _lib.check(L.cn_config_validate(ctypes.byref(self.cfg)))
         h = ctypes.c_void_p()
-        with torch.cuda.device(self.device):
-            _lib.check(L.cn_create(ctypes.byref(self.cfg), self.device.index, ctypes.byref(h)))
+        if _mixed is None:
+            self.cfg = cfg.copy()
+            self.groups = None
+            self.E, self.N = int(cfg.num_envs), int(cfg.human_num)
+            _lib.check(L.cn_config_validate(ctypes.byref(self.cfg)))
+            with torch.cuda.device(self.device):
+                _lib.check(L.cn_create(ctypes.byref(self.cfg), self.device.index, ctypes.byref(h)))
+        else:
+            cfgs, env_group = _mixed
+            arr = (abi.CnConfig * len(cfgs))(*[c.copy() for c in cfgs])
+            for c in arr:
+                if c.num_envs > 0:
+                    _lib.check(L.cn_config_validate(ctypes.byref(c)))
+            eg = np.ascontiguousarray(env_group, dtype=np.int32)
+            self.E, self.N = int(eg.size), max(int(c.human_num) for c in cfgs)
+            with torch.cuda.device(self.device):
+                _lib.check(L.cn_create_mixed(arr, len(cfgs), eg.ctypes.data_as(ctypes.c_void_p), self.E,
+                                             self.device.index, ctypes.byref(h)))
+            self.cfg = arr[0].copy()
+            self.groups = [(arr[g], np.nonzero(eg == g)[0].astype(np.int32)) for g in range(len(cfgs))
+                           if (eg == g).any()]
         self._h = h
         nb = ctypes.c_int64()
         _lib.check(L.cn_state_bytes(h, ctypes.byref(nb)))
         self.state_bytes = nb.value
         E, N, dev = self.E, self.N, self.device
+        hn = np.zeros(E, np.int32)
+        _lib.check(L.cn_env_humans(h, hn.ctypes.data_as(ctypes.c_void_p)))
+        self.env_humans = torch.from_numpy(hn).to(dev)            # (E,) humans of each env
+        self.human_mask = torch.arange(N, device=dev)[None, :] < self.env_humans[:, None]   # (E, N) real slots
         self.robot_node = torch.zeros((E, 1, 7), dtype=torch.float32, device=dev)
         self.temporal_edges = torch.zeros((E, 1, 2), dtype=torch.float32, device=dev)
         self.spatial_edges = torch.zeros((E, N, 2), dtype=torch.float32, device=dev)
@@ -48,6 +68,15 @@ class CrowdNavEngine:
         self.info = torch.zeros((E, abi.INFO_K), dtype=torch.float32, device=dev)
         self.ep_return = torch.zeros((E,), dtype=torch.float64, device=dev)
         self.ep_len = torch.zeros((E,), dtype=torch.int32, device=dev)
+
+    @classmethod
+    def mixed(cls, cfgs, env_group, device=None):
+        """One engine over envs of several configurations (cn_create_mixed): env r runs
+        cfgs[env_group[r]] (its own human count, scenarios, radius, ...). N = the largest human count;
+        spatial_edges rows past an env's own count are padding (`human_mask` False): a never-seen human
+        at the reference's unseen-belief position (15, 15). Build the configs with
+        config.make_mixed_cn_configs."""
+        return cls(None, device, _mixed=(list(cfgs), env_group))
 
     # -------------------------------------------------------------------------------------------
     def _stream(self):
@@ -90,13 +119,25 @@ class CrowdNavEngine:
         return out
 
     def get_state(self):
+        """abi.StateView of the engine; a mixed engine: [(rows, StateView of the group)] in group order."""
         buf = np.zeros(self.state_bytes, np.uint8)
         with self.torch.cuda.device(self.device):
             _lib.check(_lib.lib().cn_get_state(self._h, self._stream(), buf.ctypes.data_as(ctypes.c_void_p), 1))
-        return abi.StateView(buf, self.E, self.N, self.cfg.robot_visible)
+        if self.groups is None:
+            return abi.StateView(buf, self.E, self.N, self.cfg.robot_visible)
+        out, off = [], 0
+        for c, rows in self.groups:
+            nb = abi.state_layout(int(c.num_envs), int(c.human_num), c.robot_visible)[1]
+            out.append((rows, abi.StateView(buf[off:off + nb].copy(), int(c.num_envs), int(c.human_num),
+                                            c.robot_visible)))
+            off += nb
+        return out
 
     def set_state(self, sv):
-        blob = np.ascontiguousarray(sv.blob)
+        if self.groups is not None:
+            blob = np.concatenate([np.ascontiguousarray(v.blob).view(np.uint8).ravel() for _, v in sv])
+        else:
+            blob = np.ascontiguousarray(sv.blob)
         if blob.nbytes != self.state_bytes:
             raise ValueError("state blob has %d bytes, engine expects %d" % (blob.nbytes, self.state_bytes))
         with self.torch.cuda.device(self.device):

@@ -147,6 +147,23 @@ int cn_config_validate(const cn_config *cfg);
 int cn_create(const cn_config *cfg, int device, cn_engine **out);
 void cn_destroy(cn_engine *eng);
 
+/* Mixed engine: per-env scenario dispatch with per-env human counts in ONE engine (the
+ * reference picks a scenario per env reset, crowd_sim_dict.py:112-125, and the side-preference scenarios
+ * run with their own human count / circle radius / fixed robot, crowd_sim.py:334-357,642-651).
+ * Env r (global index env_offset + r) belongs to group env_group[r]; groups[g] is a full cn_config for
+ * its envs (num_envs = how many envs env_group assigns to g; env_offset / nenv / seed / phase equal across
+ * groups; round-robin scenario mode with the FULL scenario list, so env r's scenario
+ * scenarios[(env_offset + r) % num_scenarios] must be one group env_group[r] is configured for).
+ * The engine then behaves as one engine of num_envs envs with N = max human_num: cn_reset / cn_step take
+ * [num_envs]-row buffers; spatial_edges rows beyond an env's own human count are padding (a never-seen
+ * human: belief (15, 15) relative to the robot). cn_step launches one step kernel per group.
+ * cn_get_state / cn_set_state: the groups' blobs concatenated in group order; cn_state_device_ptr: NULL;
+ * cn_lidar_obs: CN_EUNSUPPORTED. */
+int cn_create_mixed(const cn_config *groups, int num_groups, const int32_t *env_group, int64_t num_envs, int device,
+                    cn_engine **out);
+/* per-env human count, into host memory [E] (a plain engine: N everywhere) */
+int cn_env_humans(const cn_engine *eng, int32_t *dst);
+
 /* Reset all envs (fresh episodes, case_counter continues). obs out: robot_node [E][7], temporal [E][2],
  * spatial [E][N][2] float32. */
 int cn_reset(cn_engine *eng, void *stream, float *robot_node, float *temporal_edges, float *spatial_edges);

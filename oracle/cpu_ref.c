@@ -54,6 +54,7 @@ typedef struct ref_engine {
     void *blob;
     cn_state_ptrs s;
     int64_t case_size, counter_offset;
+    int32_t *rows;       /* env e's row in a mixed engine (global index = env_offset + rows[e]); NULL: e */
 } ref_engine;
 
 /* ------------------------------------------------------------------------------------------------ */
@@ -864,7 +865,7 @@ static void gen_obs(ref_engine *g, int e, int reset, float *robot_node, float *t
 static void env_reset(ref_engine *g, int e, float *robot_node, float *temporal, float *spatial)
 {
     const int N = g->N;
-    const int64_t gidx = g->c.env_offset + e;
+    const int64_t gidx = g->c.env_offset + (g->rows ? g->rows[e] : e);
     rng_t r = {&g->s.mt[(int64_t)e * CN_MT_N], &g->s.mt_pos[e], g->c.rng_mode == CN_RNG_PHILOX};
     /* scenario choice (crowd_sim_dict.py:110-125); the unseeded random.choices is replaced by a
      * deterministic assignment (identical to the reference when one scenario is configured) */
@@ -1249,7 +1250,19 @@ EXPORT int cnref_create(const cn_config *cfg, ref_engine **out)
     *out = g;
     return 0;
 }
-EXPORT void cnref_destroy(ref_engine *g) { if (g) { free(g->blob); free(g); } }
+EXPORT void cnref_destroy(ref_engine *g) { if (g) { free(g->rows); free(g->blob); free(g); } }
+/* mixed engine group (cn_create_mixed): env e is row rows[e] of the whole engine; seeds and round-robin
+ * scenarios use the global index env_offset + rows[e] */
+EXPORT int cnref_set_rows(ref_engine *g, const int32_t *rows)
+{
+    free(g->rows);
+    g->rows = NULL;
+    if (!rows) return 0;
+    g->rows = (int32_t *)malloc(sizeof(int32_t) * (size_t)g->E);
+    if (!g->rows) return fail(CN_ENOMEM, "rows");
+    memcpy(g->rows, rows, sizeof(int32_t) * (size_t)g->E);
+    return 0;
+}
 EXPORT int64_t cnref_state_bytes(ref_engine *g) { return g->bytes; }
 EXPORT void *cnref_state_ptr(ref_engine *g) { return g->blob; }
 

@@ -23,8 +23,7 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH):
-            build()
+        build()   # make: a no-op when the library is newer than cpu_ref.c (never a stale checker)
         L = ctypes.CDLL(_LIB_PATH)
         vp, fp = ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)
         L.cnref_create.argtypes = [ctypes.POINTER(abi.CnConfig), ctypes.POINTER(vp)]
@@ -41,6 +40,7 @@ def lib():
         L.cnref_rvo2_agent0.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
                                         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp, vp]
         L.cnref_set_threads.argtypes = [ctypes.c_int]
+        L.cnref_set_rows.argtypes = [vp, vp]
         L.cnref_norm_zone_margin.restype = ctypes.c_double
         L.cnref_norm_zone_margin.argtypes = [ctypes.c_double] * 5 + [ctypes.c_int, ctypes.c_int]
         L.cnref_last_error.restype = ctypes.c_char_p
@@ -100,6 +100,66 @@ class RefEngine:
     def set_state(self, sv):
         assert sv.blob.nbytes == self.nbytes
         lib().cnref_set_state(self.h, _p(np.ascontiguousarray(sv.blob)))
+
+
+class RefMixedEngine:
+    """Oracle of the mixed engine (cn_create_mixed): one RefEngine per group whose env e is
+    row rows[e] of the whole engine (seeds / round-robin scenarios from the global index), stepped on its
+    rows' actions, outputs scattered back to the rows; spatial_edges padded to the largest human count
+    with a never-seen human (the reference's unseen belief (15, 15), crowd_sim.py:437-455, relative to
+    the robot's float64 position)."""
+
+    def __init__(self, cfgs, env_group):
+        eg = np.asarray(env_group, np.int32)
+        self.E, self.N = int(eg.size), max(int(c.human_num) for c in cfgs)
+        self.groups = []
+        for g, c in enumerate(cfgs):
+            rows = np.nonzero(eg == g)[0].astype(np.int32)
+            if rows.size == 0:
+                continue
+            assert c.num_envs == rows.size
+            eng = RefEngine(c)
+            rc = lib().cnref_set_rows(eng.h, _p(rows))
+            if rc != 0:
+                raise RuntimeError(lib().cnref_last_error().decode())
+            self.groups.append((eng, rows))
+
+    def _scatter(self, parts, reset):
+        E, N = self.E, self.N
+        obs = {"robot_node": np.zeros((E, 1, 7), np.float32), "temporal_edges": np.zeros((E, 1, 2), np.float32),
+               "spatial_edges": np.zeros((E, N, 2), np.float32)}
+        outs = None
+        for (eng, rows), p in zip(self.groups, parts):
+            o = p if reset else p[0]
+            obs["robot_node"][rows] = o["robot_node"]
+            obs["temporal_edges"][rows] = o["temporal_edges"]
+            obs["spatial_edges"][rows, :eng.N] = o["spatial_edges"]
+            if eng.N < N:
+                sv = eng.get_state()
+                rx, ry = sv.r_px, sv.r_py
+                obs["spatial_edges"][rows, eng.N:, 0] = (15.0 - rx).astype(np.float32)[:, None]
+                obs["spatial_edges"][rows, eng.N:, 1] = (15.0 - ry).astype(np.float32)[:, None]
+            if not reset:
+                if outs is None:
+                    outs = [np.zeros((E,) + a.shape[1:], a.dtype) for a in p[1:]]
+                for dst, a in zip(outs, p[1:]):
+                    dst[rows] = a
+        return obs if reset else (obs,) + tuple(outs)
+
+    def reset(self):
+        return self._scatter([eng.reset() for eng, _ in self.groups], True)
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, dtype=np.float32).reshape(self.E, 2)
+        return self._scatter([eng.step(a[rows]) for eng, rows in self.groups], False)
+
+    def get_state(self):
+        return [(rows, eng.get_state()) for eng, rows in self.groups]
+
+    def set_state(self, svs):
+        for (eng, rows), (rows2, sv) in zip(self.groups, svs):
+            assert np.array_equal(rows, rows2)
+            eng.set_state(sv)
 
 
 def mt_draw(seed, n):
