@@ -75,6 +75,8 @@ def lib():
     L.cn_debug_disc_quad.argtypes = [vp, i64, ctypes.c_int] + [vp] * 6
     L.cn_debug_orca.argtypes = [vp, i64, ctypes.c_int, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp]
     L.cn_debug_copy64.argtypes = [vp, i64, ctypes.c_int, vp, vp]
+    L.cn_orca_predict.argtypes = [vp, i64, ctypes.c_int, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp]
+    L.cn_social_force_predict.argtypes = [vp, i64, ctypes.c_int, vp, vp] + [ctypes.c_double] * 4 + [vp]
     L.cn_gru_bwd_step.argtypes = [vp, i64, ctypes.c_int] + [vp] * 7
     L.cn_lidar_obs.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, vp, vp]
     L.cn_attn_pool_fwd.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int] + [vp] * 3
@@ -84,7 +86,7 @@ def lib():
                                   ctypes.POINTER(i64)]
     for f in ("cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
               "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features", "cn_profile",
-              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64"):
+              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_social_force_predict"):
         getattr(L, f).restype = i32
     _lib = L
     return L
@@ -101,4 +103,4 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
             "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter",
             "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad",
-            "cn_debug_orca", "cn_debug_copy64"]
+            "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_social_force_predict"]

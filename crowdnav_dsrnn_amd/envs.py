@@ -32,12 +32,40 @@ _REGISTRY = {}
 
 
 def register(id, entry_point):  # noqa: A002 - gym's keyword name
-    """gym.envs.registration.register equivalent (crowd_sim/__init__.py:9-11)."""
+    """gym.envs.registration.register equivalent (crowd_sim/__init__.py:9-11): `entry_point` is a
+    "module:Class" string (or the class) of a batched env with CrowdNavVecEnv's constructor; make_vec_envs
+    resolves it like gym.make does. When gym itself is importable the id is registered there too, so
+    `gym.spec(id)` / `gym.envs.registry` list it as the reference's registration does."""
     _REGISTRY[id] = entry_point
+    try:
+        import gym  # noqa: F401  (absent in this image; optional)
+        from gym.envs.registration import register as gym_register
+    except Exception:
+        return
+    try:
+        gym_register(id=id, entry_point=entry_point)
+    except Exception:   # already registered
+        pass
 
 
 def registry():
     return dict(_REGISTRY)
+
+
+def resolve(env_name):
+    """The registered entry point of `env_name` as a class (gym's load("module:attr"))."""
+    if env_name not in _REGISTRY:
+        raise KeyError("No registered env with id: %s (registered: %s)" % (env_name, sorted(_REGISTRY)))
+    ep = _REGISTRY[env_name]
+    if not isinstance(ep, str):
+        return ep
+    import importlib
+
+    mod, _, attr = ep.partition(":")
+    obj = importlib.import_module(mod)
+    for a in attr.split("."):
+        obj = getattr(obj, a)
+    return obj
 
 
 register("CrowdSimDict-v0", "crowdnav_dsrnn_amd.envs:CrowdNavVecEnv")
@@ -49,8 +77,7 @@ def make_vec_envs(env_name, seed, num_processes, gamma, log_dir, device, allow_e
     """envs.py:106-156. `gamma` / `log_dir` are accepted for signature compatibility (VecNormalize only
     wraps Box observations, the Monitor writes no file: envs.py:79,141-146). `ax` / `fig` select the
     matplotlib rendering path, which is out of scope and rejected."""
-    if env_name not in _REGISTRY:
-        raise KeyError("No registered env with id: %s (registered: %s)" % (env_name, sorted(_REGISTRY)))
+    env_cls = resolve(env_name)
     if config is None:
         raise ValueError("config is required (CrowdSim.configure(config), envs.py:65)")
     if ax is not None or fig is not None:
@@ -61,8 +88,8 @@ def make_vec_envs(env_name, seed, num_processes, gamma, log_dir, device, allow_e
     if num_processes % world != 0:
         raise ValueError("num_processes=%d does not split over %d shards" % (num_processes, world))
     E = num_processes // world
-    return CrowdNavVecEnv(config, E, seed, device, allow_early_resets=allow_early_resets,
-                          env_offset=rank * E, nenv=num_processes, engine_device=engine_device)
+    return env_cls(config, E, seed, device, allow_early_resets=allow_early_resets,
+                   env_offset=rank * E, nenv=num_processes, engine_device=engine_device)
 
 
 class _LazyInfos:

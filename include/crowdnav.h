@@ -266,6 +266,20 @@ int cn_debug_orca(void *stream, int64_t n, int A, const float *agents, const flo
  * and store per lane, in segments of `seg` consecutive doubles per 64-lane wave (seg = 64: a field of the
  * per-human SoA arrays; seg = 6: a per-env field of one workgroup). tools/calib_pmc.py reads the
  * counters of known byte counts through it. */
+/* Agent policy plugin (replaces policy_factory[name](config).predict(JointState),
+ * crowd_nav/policy/policy_factory.py:1-17; host side crowdnav_dsrnn_amd/policy_factory.py).
+ * cn_orca_predict: ORCA.predict (crowd_nav/policy/orca.py:64-139) of n independent simulators of A <= 10
+ *   agents, arguments and outputs as cn_debug_orca (the caller keeps the simulator's frozen radii and max
+ *   speed, orca.py:85-115).
+ * cn_social_force_predict: SOCIAL_FORCE.predict (crowd_nav/policy/social_force.py:11-66) of n agents,
+ *   float64: self [n][9] = FullState (px, py, vx, vy, radius, gx, gy, v_pref, theta), others [n][M][5] =
+ *   ObservableState (px, py, vx, vy, radius), A / B / KI = config.sf, time_step = config.env.time_step;
+ *   out [n][2] = the ActionXY (vx, vy). Device pointers, stream-ordered. */
+int cn_orca_predict(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
+                    float time_horizon, float time_step, float *out);
+int cn_social_force_predict(void *stream, int64_t n, int M, const double *self, const double *others, double A,
+                            double B, double KI, double time_step, double *out);
+
 int cn_debug_copy64(void *stream, int64_t n, int seg, const double *src, double *dst);
 
 /* out[r][h] = sum_n hs[r][n][h] * attn[r][n]; hs [R][N][H], attn [R][N], out [R][H]; H % 4 == 0. */

@@ -34,6 +34,23 @@ def test_registry_and_spaces():
     assert act.__class__.__name__ == "Box" and tuple(act.shape) == (2,)
 
 
+def test_registry_resolves_entry_points():
+    """make_vec_envs builds the class the id is registered to (gym.make's "module:attr" loading)."""
+    assert envs.resolve("CrowdSimDict-v0") is envs.CrowdNavVecEnv
+    seen = {}
+
+    class Probe:
+        def __init__(self, config, E, seed, device, **kw):
+            seen.update(E=E, seed=seed, kw=kw)
+
+    envs.register("ProbeEnv-v0", Probe)
+    try:
+        envs.make_vec_envs("ProbeEnv-v0", 3, 4, 0.99, None, "cpu", False, config=_config(), shard=(1, 2))
+        assert seen["E"] == 2 and seen["seed"] == 3 and seen["kw"]["env_offset"] == 2 and seen["kw"]["nenv"] == 4
+    finally:
+        envs._REGISTRY.pop("ProbeEnv-v0")
+
+
 def test_rejects_out_of_scope_options():
     with pytest.raises(NotImplementedError):
         envs.make_vec_envs("CrowdSimDict-v0", 0, 1, 0.99, None, "cpu", False, config=_config(), ax=object())
