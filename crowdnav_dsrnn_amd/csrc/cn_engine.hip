@@ -1,14 +1,18 @@
 // cn_engine.hip — MI355X (gfx950) batched CrowdSimDict engine: kernels + C ABI (include/crowdnav.h).
 //
 // Hot path: ONE kernel launch per cn_step (no host synchronisation, no second kernel):
-//   cn_step_kernel, workgroups [0, step_blocks): one lane per (env, human), 256-lane workgroups holding
+//   cn_step_kernel, step workgroups: one lane per (env, human), 256-lane workgroups holding
 //       floor(256/N) whole envs. Phases 0-4: SRNN.clip_action, the human policies (ORCA LP / social
 //       force) on the PRE-move state, calc_reward, kinematics, observation, Monitor. Phase 5: the
 //       workgroup's own RNG work, one wave per env needing it — goal changes (numpy-legacy MT19937 in
 //       LDS) and the VecEnv auto-reset, which copies a spawn drawn ahead of time.
-//   cn_step_kernel, workgroups [step_blocks, +pend_blocks): spawn waves. CrowdSimDict.reset is a pure
-//       function of the seed schedule, so each env's NEXT episode is drawn (reseed + spawn with
-//       rejection) by these spare workgroups right after its reset, concurrently with the step.
+//   cn_step_kernel, spare workgroups: spawn waves. CrowdSimDict.reset is a pure function of the seed
+//       schedule, so each env's NEXT episode is drawn (reseed + spawn with rejection) by these spare
+//       workgroups right after its reset, concurrently with the step. On the kd-tree path they come
+//       first in the grid so that they are dispatched first: a crowded spawn (25 humans in
+//       square_crossing) runs ~1M cycles, longer than the step workgroups' rounds, and started last it
+//       would add its whole latency to the launch. On the quad path (cheap spawns) they come last, so
+//       the step workgroups start without waiting for their dispatch.
 //   cn_reset_kernel: cn_reset (every env), one wave per env.
 // Reference: crowd_sim/envs/crowd_sim_dict.py:105-271, crowd_sim/envs/crowd_sim.py:296-1161,
 // crowd_sim/envs/utils/agent.py:172-218, crowd_nav/policy/{orca,social_force,srnn}.py; RVO2 v2.0
@@ -45,7 +49,7 @@ __device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_c[8192 * 4];   // crowded rejection: ensure / cand / test / passes
 __device__ unsigned long long cn_stamp_p[8192 * 2];   // spawn waves: start / end of each env's latest spawn
-#define STAMP_A(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + (k)] = clock64(); } while (0)
+#define STAMP_A(k) do { const unsigned sb_ = (unsigned)sb; if (threadIdx.x == 0 && sb_ < 4096) cn_stamp_a[sb_ * CN_NSTAMP + (k)] = clock64(); } while (0)
 #define STAMP_B(w, k) do { if ((threadIdx.x & 63) == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
 #else
 #define STAMP_A(k) do { } while (0)
@@ -977,8 +981,8 @@ __device__ int wave_reject2(WRng &m, int W, int NA, int max_tries, uint32_t &ovf
 // bounding box (4 cells per lane, float32 with a 1e-4 m margin, so the binning is conservative): a cell
 // lying inside some disc rejects every try that lands in it, a try outside the box hits nothing, and
 // otherwise only the agents overlapping its cell are tested exactly (norm_lt). Same result as testing
-// every agent. (The goal rejection keeps the plain test: binning there measured no gain in C3 and cost
-// the quad path 8 % in code size.)
+// every agent. The crowded goal rejection (goal_reject_crowded<GRID>) uses it on the kd-tree path only
+// (the quad path's scenes are sparse and its code stays smaller).
 struct DiscGrid {
     uint32_t *mask;   // [256] per cell: bit a = agent a's position or goal disc overlaps the cell (NA <= 32)
     uint64_t *cov;    // [4] bit = cell entirely inside some disc
@@ -1129,7 +1133,11 @@ __device__ int wave_reject_discs(WRng &m, int W, int NA, int max_tries, uint32_t
 // precomputed, and each lane tests them four at a time with the loads of a group issued together (the
 // agent-at-a-time loop was bound by dependent LDS latency). Same result as goal_hit over the tries in
 // order; returns the winning slot (m.sl[t], m.sl[64 + t]), m.p after its words.
-template <typename FC>
+// GRID (the kd-tree path, whose waves have DiscGrid space in m.grid): the position and goal discs of the
+// agents are binned once per loop (disc_grid_build<true>) and each try tests only its cell's agents --
+// at 25 humans in square_crossing most of these loops run all max_tries = 1000 tries (16 passes), so the
+// one-off binning is repaid many times over; same result.
+template <bool GRID, typename FC>
 __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, int self, double r_self, int W,
                                    int max_tries, uint32_t &ovf, FC cand)
 {
@@ -1145,6 +1153,15 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
         tmd[lane] = r_self + ar + c.discomfort_dist;
     }
     wsync();
+    DiscGrid gr;
+    const bool grid = GRID && m.grid && NA >= 8;
+    if (grid) {
+        gr.mask = (uint32_t *)(m.grid + 96 * 8);
+        gr.cov = (uint64_t *)(m.grid + 96 * 8 + CN_GRID * CN_GRID * 4);
+        gr.par = (double *)(gr.cov + 4);
+        disc_grid_build<true>(gr, tx, ty, tgx, tgy, tmd, NA, lane);
+        wsync();
+    }
     const int J = min(64, CN_MT_N / W);
 #ifdef CN_STAMPS
     unsigned long long tq = clock64(), tc_e = 0, tc_c = 0, tc_t = 0, tc_n = 0;
@@ -1165,6 +1182,8 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
         { const unsigned long long t_ = clock64(); tc_c += t_ - tq; tq = t_; }
 #endif
         bool bad = lane >= nt;
+        if (grid) bad = bad || disc_grid_hit<true>(gr, tx, ty, tgx, tgy, tmd, gx, gy);
+        else
         for (int a0 = 0; a0 < NA && !bad; a0 += 4) {
             double x[4], y[4], u[4], v[4], d[4];
 #pragma unroll
@@ -1402,7 +1421,7 @@ __device__ __forceinline__ void gpage_build(WRng &m, GPage &pg, bool trig)
 // the walk itself is wave-uniform table reads; a changing human tests J tries at once, lane = (try t,
 // agent a), against the robot and the other humans (earlier humans already carry their new goals); the
 // first try without a hit wins. Bounded by max_tries like every rejection loop.
-template <int KIND>
+template <int KIND, bool GRID>
 __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, uint32_t &ovf, int sc, double *sp,
                                          int64_t edbg = -1)
 {
@@ -1457,7 +1476,7 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
             if (t0 > 0) {
                 // crowded (the first batch was all rejected): the remaining tries 64 candidates at a time
                 // straight from the stream (goal_reject_crowded); its try slots overwrite the page
-                const int tw = goal_reject_crowded(c, en, m, h, r_self, W, c.max_tries - t0, ovf, [&](int q, int tt) {
+                const int tw = goal_reject_crowded<GRID>(c, en, m, h, r_self, W, c.max_tries - t0, ovf, [&](int q, int tt) {
                     double gx, gy;
                     if (KIND == 0) {
                         gx = c.circle_radius * m.cos2pi(q) + (m.dbl(q + 2) - 0.5) * vpk;
@@ -1525,6 +1544,7 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
 // update_human_goals_randomly when `rgoal`, then update_human_goal when `egoal` (goal_pass).
 // `en` holds the post-move agents (LDS); the env's MT19937 stream is loaded from / written back to
 // the state; `sp` = wave LDS scratch.
+template <bool GRID>
 __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_ptrs &S, int64_t e, Env1 &en, WRng &m,
                                              bool rgoal, bool egoal, double *sp)
 {
@@ -1548,9 +1568,9 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
     wsync();
     STAMP_B(e, 1);
     int dbg0 = 0, dbg1 = 0;
-    if (rgoal) dbg0 = goal_pass<0>(c, en, m, ovf, sc, sp, e);
+    if (rgoal) dbg0 = goal_pass<0, GRID>(c, en, m, ovf, sc, sp, e);
     STAMP_B(e, 2);
-    if (egoal) dbg1 = goal_pass<1>(c, en, m, ovf, sc, sp, e);
+    if (egoal) dbg1 = goal_pass<1, GRID>(c, en, m, ovf, sc, sp, e);
     STAMP_B(e, 3);
 #ifdef CN_STAMPS
     if (lane == 0 && e < 8192) { cn_stamp_b[e * CN_NSTAMP + 6] = dbg0; cn_stamp_b[e * CN_NSTAMP + 7] = dbg1; }
@@ -1614,6 +1634,7 @@ struct PendLaunch {
     const uint32_t *count;
     int all;                // 1: every env (list ignored)
     int step_blocks, pend_blocks;
+    int first;              // 1: workgroups [0, pend_blocks) (kd-tree path); 0: after the step workgroups
     int waves;              // spawning waves per spare workgroup (RNG regions that fit the launch's LDS)
     int stride;             // bytes per spawning wave's region (StepPlan::rng_stride)
     int64_t counter_offset;
@@ -1632,8 +1653,9 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
     double *hb = (double *)(base + 2 * CN_MT_N * 4);
     // envs reset by the previous launch: the reset after next (the next one was drawn earlier); after
     // cn_reset / cn_set_state (all): both the next (items [0, E)) and the one after ([E, 2E))
-    const uint32_t n = pl.all ? (uint32_t)(2 * E) : *pl.count;
-    for (uint32_t it = (uint32_t)((blockIdx.x - pl.step_blocks) * nw + w); it < n; it += (uint32_t)(pl.pend_blocks * nw)) {
+    const uint32_t n = pl.all ? (uint32_t)(2 * E) : min(*pl.count, (uint32_t)E);
+    const int pb = pl.first ? (int)blockIdx.x : (int)blockIdx.x - pl.step_blocks;
+    for (uint32_t it = (uint32_t)(pb * nw + w); it < n; it += (uint32_t)(pl.pend_blocks * nw)) {
         const int64_t e = pl.all ? (int64_t)(it % (uint32_t)E) : (int64_t)pl.list[it];
         const bool ahead2 = !pl.all || it >= (uint32_t)E;
         Env1 en;
@@ -1679,7 +1701,7 @@ struct StepArgs {
     uint32_t *plist_w;      // envs reset by this launch (their next spawn is drawn by the next launch)
     uint32_t *pcount_w;
     uint32_t *pcount_zero;  // the counter the NEXT launch appends to (triple-buffered), zeroed here
-    PendLaunch pend;        // spawn waves: workgroups [step_blocks, step_blocks + pend_blocks)
+    PendLaunch pend;        // spawn waves: the first or the last pend_blocks workgroups (pend.first)
     int64_t case_size;
     int E;
     OutView ov;             // output rows / human stride (mixed engines); also pend.ov
@@ -1718,15 +1740,22 @@ __device__ inline float bbox_dist(float x, float y, float mnx, float mxx, float 
 
 // KD: RVO2 kd-tree neighbour order (> 10 agents per simulator); PHX: c.rng_mode == CN_RNG_PHILOX, a
 // template argument so that the MT19937 build carries no Philox registers
-template <bool KD, bool PHX>
+// MIX: a group of a mixed engine (outputs through g.ov); a plain engine's identity view is then a
+// compile-time constant and costs no registers
+template <bool KD, bool PHX, bool MIX>
 __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g, cn_config c)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if ((int)blockIdx.x >= g.pend.step_blocks) {  // spare workgroups: draw upcoming episodes' spawns
-        pend_waves<PHX, KD>(g.pend, g.s, c, g.E, smem);
+    const OutView ov = MIX ? g.ov : OutView{nullptr, c.human_num};
+    // the spawn-list counter the NEXT launch appends to (neither read nor appended to by this launch)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *g.pcount_zero = 0u;
+    const int sb = (int)blockIdx.x - (g.pend.first ? g.pend.pend_blocks : 0);   // step workgroup index
+    if (sb < 0 || sb >= g.pend.step_blocks) {  // spare workgroups: draw upcoming episodes' spawns
+        PendLaunch pl = g.pend;
+        pl.ov = ov;
+        pend_waves<PHX, KD>(pl, g.s, c, g.E, smem);
         return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) *g.pcount_zero = 0u;
     const int N = c.human_num;
     const StepPlan P = cn_step_plan(N, c.robot_visible);
     const int EPB = P.EPB, M = P.M, A = P.A;
@@ -1756,8 +1785,9 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     // give each XCD a contiguous run of env blocks. Neighbouring workgroups share the 128-B lines at the
     // ends of their SoA segments (a per-env field of one workgroup is only 48 B); on one XCD the second
     // reader hits in that XCD's L2 instead of fetching the line again.
-    const int nbk = g.pend.step_blocks, xq = nbk >> 3, xr = nbk & 7, xi = (int)blockIdx.x & 7;
-    const int blk = xi * xq + min(xi, xr) + ((int)blockIdx.x >> 3);
+    // (a leading pend_blocks is a multiple of 8, so step workgroup sb runs on XCD sb % 8 as well)
+    const int nbk = g.pend.step_blocks, xq = nbk >> 3, xr = nbk & 7, xi = sb & 7;
+    const int blk = xi * xq + min(xi, xr) + (sb >> 3);
     const int e0 = blk * EPB;
     const int nenv_here = min(EPB, g.E - e0);
     const int el = tid / N, i = tid - el * N;
@@ -1800,7 +1830,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         rv[R_LAX] = S.last_ax[ge]; rv[R_LAY] = S.last_ay[ge]; rv[R_EPR] = S.ep_return[ge];
         const uint32_t fl = S.flags[ge];
         pre_epl = S.ep_len[ge]; pre_sc = S.scenario[ge]; pre_ovf = S.overflow[ge];
-        const int64_t oa = orow(g.ov, ge);   // the env's row in the caller's buffers
+        const int64_t oa = orow(ov, ge);   // the env's row in the caller's buffers
         float a0 = g.actions[oa * 2], a1 = g.actions[oa * 2 + 1];
         asm volatile("" ::: "memory");
         RF(sl, R_PX, re, EPB) = rv[R_PX]; RF(sl, R_PY, re, EPB) = rv[R_PY];
@@ -2343,7 +2373,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             else reward = (double)(((float)reward + r_spin) + r_back);
         }
         if (g.info) {
-            float *info = g.info + orow(g.ov, ge) * CN_INFO_K;
+            float *info = g.info + orow(ov, ge) * CN_INFO_K;
             info[CN_INFO_AGG_NAV_TIME] = (float)agg;
             info[CN_INFO_PATH_VIOLATION] = (float)vr_viol;
             info[CN_INFO_PERSONAL_VIOLATION] = dmin < c.min_personal_space ? 1.0f : 0.0f;
@@ -2368,7 +2398,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const double epr = RF(sl, R_EPR, re, EPB) + reward;
         const int32_t epl = pre_epl + 1;
         S.ep_return[ge] = epr; S.ep_len[ge] = epl;
-        const int64_t oe = orow(g.ov, ge);
+        const int64_t oe = orow(ov, ge);
         if (g.reward) g.reward[oe] = (float)reward;
         if (g.done) g.done[oe] = (uint8_t)done;
         if (g.event) g.event[oe] = (int8_t)event;
@@ -2402,7 +2432,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             bpx = HF(sl, H_BPX, tid) + bvx * dt; bpy = HF(sl, H_BPY, tid) + bvy * dt;
         }
         S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = bvx; S.b_vy[gh] = bvy; S.b_r[gh] = br;
-        const int64_t oh = orow(g.ov, e0 + el) * g.ov.NS + i;
+        const int64_t oh = orow(ov, e0 + el) * ov.NS + i;
         g.spatial[oh * 2] = (float)(bpx - rnx);
         g.spatial[oh * 2 + 1] = (float)(bpy - rny);
         uint32_t f = sl.lf[tid] & ~LF_ENDGOAL;
@@ -2431,16 +2461,16 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         }
         if (nan) flags |= CN_FLAG_NAN;
         S.flags[ge] = flags;
-        const int64_t oe = orow(g.ov, ge);
+        const int64_t oe = orow(ov, ge);
         float *rn = g.robot_node + oe * 7;
         rn[0] = (float)nx; rn[1] = (float)ny; rn[2] = (float)RF(sl, R_RAD, re, EPB);
         rn[3] = (float)RF(sl, R_GX, re, EPB); rn[4] = (float)RF(sl, R_GY, re, EPB);
         rn[5] = (float)RF(sl, R_VP, re, EPB); rn[6] = (float)RF(sl, R_TH, re, EPB);
         g.temporal[oe * 2] = (float)RF(sl, R_VX, re, EPB);
         g.temporal[oe * 2 + 1] = (float)RF(sl, R_VY, re, EPB);
-        for (int k = N; k < g.ov.NS; ++k) {   // padding slots of a mixed engine (never-seen humans)
-            g.spatial[(oe * g.ov.NS + k) * 2] = (float)(CN_PAD_POS - nx);
-            g.spatial[(oe * g.ov.NS + k) * 2 + 1] = (float)(CN_PAD_POS - ny);
+        for (int k = N; k < ov.NS; ++k) {   // padding slots of a mixed engine (never-seen humans)
+            g.spatial[(oe * ov.NS + k) * 2] = (float)(CN_PAD_POS - nx);
+            g.spatial[(oe * ov.NS + k) * 2 + 1] = (float)(CN_PAD_POS - ny);
         }
         // random numbers needed? (crowd_sim_dict.py:260-269, shmem_vec_env.py:166-167)
         const bool done = sl.rflag[EPB + re] != 0;
@@ -2466,7 +2496,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         double *hb = (double *)(wb + 2 * CN_MT_N * 4);
         ResetOut o;
         o.s = S; o.robot_node = g.robot_node; o.temporal = g.temporal; o.spatial = g.spatial; o.case_size = g.case_size;
-        o.ov = g.ov;
+        o.ov = ov;
         // waves without an env to serve skip the block entirely: the loop's preheader (values the
         // compiler hoists out of the RNG work, and their spill stores) then runs only where it is needed
         bool mine = false;
@@ -2489,7 +2519,10 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 en.hth = hb + 192;
                 const bool may = !g.pend.all;   // both pending slots are ready unless this launch draws all
                 reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, m, en);
-                if (lane == 0) g.plist_w[atomicAdd(g.pcount_w, 1u)] = (uint32_t)e;
+                if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
+                    const uint32_t k = atomicAdd(g.pcount_w, 1u);
+                    if (k < (uint32_t)g.E) g.plist_w[k] = (uint32_t)e;
+                }
                 STAMP_B(e, 5);
             } else {
                 const int b = q * N;
@@ -2500,7 +2533,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 // update_human_goal checks every human AFTER the random changes (a new random goal may
                 // land within reach of its own human), so it runs whenever end goal changing is on
                 m.edbg = e;
-                goal_changes(c, S, e, en, m, (need & 2u) != 0, c.end_goal_changing != 0, hb);
+                goal_changes<KD>(c, S, e, en, m, (need & 2u) != 0, c.end_goal_changing != 0, hb);
             }
         }
         }
@@ -2987,8 +3020,11 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         g->pend_waves = fit < g->plan.T / 64 ? fit : g->plan.T / 64;
         const int nw = g->pend_waves;
         const int64_t need = (E + nw - 1) / nw;
-        const int cap = 128 / nw;   // ~128 spawning waves; leaves the step workgroups co-resident
-        g->pend_blocks = (int)(need < cap ? need : cap);
+        // ~128 spawning waves on the quad path; 256 on the kd-tree path, whose crowded spawns (~1M cycles
+        // each at 25 humans in square_crossing, ~4 % of the envs per step) must not queue behind each other
+        const int cap = (g->plan.kd ? 256 : 128) / nw;
+        const int pb = (int)(need < cap ? need : cap);
+        g->pend_blocks = g->plan.kd ? (pb + 7) & ~7 : pb;   // leading: a multiple of 8 (XCD placement)
     }
     cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
     // unit-circle table of GEOS's 64-gon point buffer (norm zones)
@@ -3001,8 +3037,10 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     }
     if (g->a_lds > 160 * 1024) { cn_destroy(g); return set_err(CN_EUNSUPPORTED, "LDS plan exceeds 160 KiB"); }
     if (g->a_lds > 64 * 1024) {
-        const void *ks[4] = {(const void *)cn_step_kernel<true, false>, (const void *)cn_step_kernel<false, false>,
-                             (const void *)cn_step_kernel<true, true>, (const void *)cn_step_kernel<false, true>};
+        const void *ks[8] = {(const void *)cn_step_kernel<true, false, false>, (const void *)cn_step_kernel<false, false, false>,
+                             (const void *)cn_step_kernel<true, true, false>, (const void *)cn_step_kernel<false, true, false>,
+                             (const void *)cn_step_kernel<true, false, true>, (const void *)cn_step_kernel<false, false, true>,
+                             (const void *)cn_step_kernel<true, true, true>, (const void *)cn_step_kernel<false, true, true>};
         for (const void *k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g->a_lds);
     }
     g->rng_grid = g->E < 2048 ? g->E : 2048;
@@ -3203,6 +3241,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.pend.P = g->pend; a.pend.list = g->plist + (int64_t)kr * (g->E + 64); a.pend.count = g->work_count + 2 + kr;
     a.pend.all = g->pend_all;
     a.pend.step_blocks = blocks; a.pend.pend_blocks = g->pend_blocks; a.pend.counter_offset = g->counter_offset;
+    a.pend.first = g->plan.kd ? 1 : 0;
     a.pend.waves = g->pend_waves;
     a.pend.stride = g->plan.rng_stride;
     a.pend.case_size = g->case_size;
@@ -3211,14 +3250,12 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     g->pend_all = 0;
     const int grid = blocks + g->pend_blocks;
     const bool phx = g->c.rng_mode == CN_RNG_PHILOX;
-    if (g->plan.kd && phx)
-        hipLaunchKernelGGL((cn_step_kernel<true, true>), dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
-    else if (g->plan.kd)
-        hipLaunchKernelGGL((cn_step_kernel<true, false>), dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
-    else if (phx)
-        hipLaunchKernelGGL((cn_step_kernel<false, true>), dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
-    else
-        hipLaunchKernelGGL((cn_step_kernel<false, false>), dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
+    const int variant = (g->plan.kd ? 4 : 0) | (phx ? 2 : 0) | (g->rows ? 1 : 0);
+    void (*const kern[8])(StepArgs, cn_config) = {
+        cn_step_kernel<false, false, false>, cn_step_kernel<false, false, true>, cn_step_kernel<false, true, false>,
+        cn_step_kernel<false, true, true>,   cn_step_kernel<true, false, false>,  cn_step_kernel<true, false, true>,
+        cn_step_kernel<true, true, false>,   cn_step_kernel<true, true, true>};
+    hipLaunchKernelGGL(kern[variant], dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
     HIPCHK(hipGetLastError());
     if (prof && ++g->prof_n == g->prof_cap) HIPCHK(hipEventRecord(g->ev[1], st));
     return CN_OK;

@@ -218,3 +218,42 @@ def test_gpu_free_running_matches_oracle_short_horizon(gpu, oracle, rng, shape):
         d["post_mt_crc"] = H.mt_crc(rs)
         errs = H.compare_state(gs, d, "post_", tol=1e-5)
         assert not errs, errs
+
+
+def test_gpu_full_size_c2_free_running(gpu, oracle):
+    """BASELINE config 2 at its full size (4096 envs x 10 humans, the bench workload) for 400 free-running
+    steps: the first 50 steps identical to the oracle (done / event exact, rewards 1e-5; the oracle on all
+    host threads), then size-independent properties over the whole run: finite outputs, done exactly
+    where the event is terminal, Monitor lengths within the time limit, and episode counts / mean return
+    within 2 % of the oracle's over the same 400 steps (spawn lists, pending-spawn slots and their
+    counters are exercised for hundreds of launches)."""
+    cfg = _cfg(10, "unicycle", E=4096)
+    oracle.lib().cnref_set_threads(min(16, os.cpu_count() or 1))
+    ref, g = oracle.RefEngine(cfg), gpu(cfg)
+    ref.reset()
+    g.reset()
+    rng = np.random.RandomState(3)
+    term = np.isin(np.arange(5), [abi.EV_COLLISION, abi.EV_REACHGOAL, abi.EV_TIMEOUT])
+    n_ep = [0, 0]
+    ret = [0.0, 0.0]
+    tmax = int(round(cfg.time_limit / cfg.time_step)) + 1
+    for t in range(400):
+        a = rng.uniform(-0.1, 0.1, (4096, 2)).astype(np.float32)
+        r1, r2 = ref.step(a), g.step(a)
+        if t < 50:
+            np.testing.assert_array_equal(r2[2], r1[2], err_msg="done t=%d" % t)
+            np.testing.assert_array_equal(r2[3], r1[3], err_msg="event t=%d" % t)
+            np.testing.assert_allclose(r2[1], r1[1], atol=1e-5, rtol=0, err_msg="reward t=%d" % t)
+        for k in r2[0]:
+            assert np.isfinite(r2[0][k]).all(), (k, t)
+        assert np.isfinite(r2[1]).all()
+        d = r2[2].astype(bool)
+        np.testing.assert_array_equal(d, term[r2[3]], err_msg="done vs event t=%d" % t)
+        assert (r2[6][d] >= 1).all() and (r2[6][d] <= tmax).all(), t
+        for k, r in enumerate((r1, r2)):
+            dd = r[2].astype(bool)
+            n_ep[k] += int(dd.sum())
+            ret[k] += float(r[5][dd].sum())
+    assert n_ep[1] > 1000, n_ep
+    assert abs(n_ep[1] - n_ep[0]) <= 0.02 * n_ep[0], n_ep
+    assert abs(ret[1] / n_ep[1] - ret[0] / n_ep[0]) <= 0.02 * abs(ret[0] / n_ep[0]) + 0.05, (ret, n_ep)
