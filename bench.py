@@ -202,6 +202,39 @@ def load_pmc(kernel="cn_step_kernel", workload="c2"):
             "active_inst_frac": d.get("active_inst_frac"), "avg_duration_ns": d.get("avg_duration_ns")}
 
 
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_{32x32x2,16x16x4}_f32, dense, no TF32 on gfx950
+
+
+def gru_gemm_roofline(torch, device, B, H, reps=50):
+    """Roofline of C4's dominant kernel: the per-step recurrent GEMM of the spatial-edge GRU in the PPO
+    update (ops._MaskedGRU: gh = hm W_hh^T + b_hh, B = envs per minibatch x humans rows, K = H = 256,
+    3H = 768 columns; 128 steps x 5 epochs x 2 minibatches per update, plus the backward's acc += dgh
+    W_hh of the same size). The same call on the same shapes is timed with HIP events on the stream it
+    runs on; algorithmic FLOP per launch = 2 B H 3H."""
+    g = torch.Generator(device=device)
+    g.manual_seed(1)
+    hm = torch.randn((B, H), generator=g, device=device)
+    w = torch.randn((3 * H, H), generator=g, device=device) * 0.05
+    b = torch.randn((3 * H,), generator=g, device=device)
+    out = torch.empty((B, 3 * H), device=device)
+    for _ in range(5):
+        torch.addmm(b, hm, w.t(), out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        torch.addmm(b, hm, w.t(), out=out)
+    e1.record()
+    e1.synchronize()
+    dt = e0.elapsed_time(e1) / 1e3 / reps
+    flop = 2.0 * B * H * 3 * H
+    tf = flop / dt / 1e12
+    return {"bound": "mfma", "achieved": round(tf, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+            "kernel": "spatial-edge GRU step GEMM gh = hm W_hh^T + b_hh (hipBLASLt fp32 MFMA), %d x %d -> %d"
+                      % (B, H, 3 * H),
+            "flop_per_launch": flop, "avg_launch_us": round(dt * 1e6, 2)}
+
+
 def run_c4(args, torch, dist, device, rank, world):
     """env-steps/s over PPO updates, counted like train.py:342-352 (rollout of num_steps
     steps of every env with DSRNN act() in the loop, then the PPO update, all inside the timed region).
@@ -259,6 +292,7 @@ def run_c4(args, torch, dist, device, rank, world):
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    roof = gru_gemm_roofline(torch, device, E // c.ppo.num_mini_batch * N, 256) if rank == 0 else None
     if rank == 0:
         steps_per_update = c.ppo.num_steps * E
         line = {
@@ -271,7 +305,7 @@ def run_c4(args, torch, dist, device, rank, world):
                        "global_envs": E * world, "env_steps_per_update": steps_per_update * world,
                        "rollout_s_per_update": round(roll / K, 4), "ppo_s_per_update": round(upd / K, 4),
                        "parallelism": "dp%d (env-sharded, PPO grads all-reduced)" % world},
-            "roofline": None,
+            "roofline": roof,
         }
         print(json.dumps(line), flush=True)
     envs.close()
