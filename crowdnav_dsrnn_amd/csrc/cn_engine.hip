@@ -2798,6 +2798,8 @@ struct cn_engine {
     // N = NS = the largest human count
     int ngroups;
     cn_engine **grp;
+    hipStream_t *gstream;   // [ngroups]: group k > 0 steps on gstream[k] (forked from / joined to the caller's)
+    hipEvent_t *gev;        // [ngroups + 1]: fork, then one join event per forked group
 };
 
 static thread_local char g_err[512];
@@ -3106,6 +3108,21 @@ int cn_create_mixed(const cn_config *groups, int num_groups, const int32_t *env_
         }
         m->state_bytes += g->state_bytes;
     }
+    // the groups' step launches are independent (disjoint envs and output rows): run them concurrently,
+    // group 0 on the caller's stream, group k > 0 on its own stream forked after the caller's prior work
+    // and joined back before the caller's next work (stream order is kept for the caller)
+    m->gstream = new hipStream_t[m->ngroups]();
+    m->gev = new hipEvent_t[m->ngroups + 1]();
+    for (int k = 0; k <= m->ngroups; ++k)
+        if (hipEventCreateWithFlags(&m->gev[k], hipEventDisableTiming) != hipSuccess) {
+            cn_destroy(m);
+            return set_err(CN_EHIP, "hipEventCreate failed");
+        }
+    for (int k = 1; k < m->ngroups; ++k)
+        if (hipStreamCreateWithFlags(&m->gstream[k], hipStreamNonBlocking) != hipSuccess) {
+            cn_destroy(m);
+            return set_err(CN_EHIP, "hipStreamCreate failed");
+        }
     *out = m;
     return CN_OK;
 }
@@ -3173,9 +3190,15 @@ void cn_destroy(cn_engine *g)
     if (!g) return;
     (void)hipSetDevice(g->device);
     prof_free(g);
-    if (g->ngroups) {
+    if (g->grp) {
         for (int k = 0; k < g->ngroups; ++k) cn_destroy(g->grp[k]);
+        if (g->gstream)
+            for (int k = 1; k < g->ngroups; ++k) (void)hipStreamDestroy(g->gstream[k]);
+        if (g->gev)
+            for (int k = 0; k <= g->ngroups; ++k) (void)hipEventDestroy(g->gev[k]);
         delete[] g->grp;
+        delete[] g->gstream;
+        delete[] g->gev;
         delete g;
         return;
     }
@@ -3220,12 +3243,17 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     ++g->nstep;
     const bool prof = g->prof_on && g->prof_n < g->prof_cap;
     if (prof && g->prof_n == 0) HIPCHK(hipEventRecord(g->ev[0], st));
-    if (g->ngroups) {   // one step launch per group, back to back on the stream
+    if (g->ngroups) {   // one step launch per group, concurrently (fork / join around the caller's stream)
+        if (g->ngroups > 1) HIPCHK(hipEventRecord(g->gev[0], st));
         for (int k = 0; k < g->ngroups; ++k) {
-            const int rc = cn_step(g->grp[k], stream, actions, robot_node, temporal, spatial, reward, done, event, info,
-                                   ep_return, ep_len);
+            hipStream_t sk = st;
+            if (k > 0) { sk = g->gstream[k]; HIPCHK(hipStreamWaitEvent(sk, g->gev[0], 0)); }
+            const int rc = cn_step(g->grp[k], (void *)sk, actions, robot_node, temporal, spatial, reward, done, event,
+                                   info, ep_return, ep_len);
             if (rc) return rc;
+            if (k > 0) HIPCHK(hipEventRecord(g->gev[k], sk));
         }
+        for (int k = 1; k < g->ngroups; ++k) HIPCHK(hipStreamWaitEvent(st, g->gev[k], 0));
         if (prof && ++g->prof_n == g->prof_cap) HIPCHK(hipEventRecord(g->ev[1], st));
         return CN_OK;
     }
