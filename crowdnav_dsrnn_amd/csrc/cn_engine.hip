@@ -184,7 +184,14 @@ __device__ __forceinline__ int vis360(bool heading_finite, double px1, double py
     const double n2 = __fma_rn(dy, dy, dx * dx);
     return (n2 > 1e-300 && n2 < 1e300) ? 1 : -1;
 }
-__device__ inline bool in_fov(double fx, double fy, double px1, double py1, double px2, double py2, double fov)
+// arccos(d) <= fov / 2, the reference's test, out of line: only cosines within the band below reach it
+__device__ __noinline__ bool acos_within(double d, double fov) { return fabs(acos(d)) <= fov / 2; }
+// `cth` = cos(fov / 2) (any accurate evaluation): arccos is decreasing with |d arccos / dd| >= 1, so for
+// |d - cth| > 1e-12 the arccos of d is farther than 1e-12 from fov / 2 -- orders of magnitude beyond the
+// few-ulp error of any arccos or cosine -- and the comparison of d with cth gives the arccos test's
+// answer; only the 2e-12-wide band around cth evaluates the arccos itself.
+__device__ inline bool in_fov(double fx, double fy, double px1, double py1, double px2, double py2, double fov,
+                              double cth)
 {
     double vx = px2 - px1, vy = py2 - py1;
     const double nv = np_norm2(vx, vy);
@@ -193,7 +200,9 @@ __device__ inline bool in_fov(double fx, double fy, double px1, double py1, doub
     if (d != d) return false;  // coincident agents: arccos(nan) -> not visible
     if (fov >= 2.0 * CN_PI) return true;
     d = d < -1.0 ? -1.0 : (d > 1.0 ? 1.0 : d);
-    return fabs(acos(d)) <= fov / 2;
+    if (d > cth + 1e-12) return true;
+    if (d < cth - 1e-12) return false;
+    return acos_within(d, fov);
 }
 
 // the robot's FOV test of a freshly spawned human (generate_ob(reset=True)), out of line: inlined into the
@@ -203,7 +212,7 @@ __device__ __noinline__ int reset_fov_test(double th, double rpx, double rpy, do
 {
     double fx, fy;
     fov_dir64(th, fx, fy);
-    return in_fov(fx, fy, rpx, rpy, px, py, fov) ? 1 : 0;
+    return in_fov(fx, fy, rpx, rpy, px, py, fov, cos(fov / 2)) ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1705,6 +1714,7 @@ struct StepArgs {
     int64_t case_size;
     int E;
     OutView ov;             // output rows / human stride (mixed engines); also pend.ov
+    double cth_h, cth_r;    // cos(human_fov / 2), cos(robot_fov / 2): in_fov's thresholds
 };
 
 // observed agent of slot k seen by lane (human i of env base eb): position/velocity float32,
@@ -1963,14 +1973,14 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         for (int k = 0; k < N - 1; ++k) {
             const int j = eb + (k < i ? k : k + 1);
             int v = full ? vis360(hfin, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j)) : -1;
-            if (v < 0) { dir(); v = in_fov(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov) ? 1 : 0; }
+            if (v < 0) { dir(); v = in_fov(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov, g.cth_h) ? 1 : 0; }
             if (v) vis |= 1u << k;
         }
         if (c.robot_visible) {
             int v = full ? vis360(hfin, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB)) : -1;
             if (v < 0) {
                 dir();
-                v = in_fov(fx, fy, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB), c.human_fov) ? 1 : 0;
+                v = in_fov(fx, fy, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB), c.human_fov, g.cth_h) ? 1 : 0;
             }
             if (v) vis |= 1u << (N - 1);
         }
@@ -2422,7 +2432,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             double fx, fy;
             if (holo) fov_dir32(atan2f(rvy, rvx), fx, fy);
             else fov_dir32((float)RF(sl, R_TH, el, EPB), fx, fy);
-            rv = in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov) ? 1 : 0;
+            rv = in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov, g.cth_r) ? 1 : 0;
         }
         double bpx, bpy, bvx, bvy, br;
         if (rv) {
@@ -2802,6 +2812,17 @@ struct cn_engine {
     hipEvent_t *gev;        // [ngroups + 1]: fork, then one join event per forked group
 };
 
+// unit-circle table of GEOS's 64-gon point buffer (norm zones), per device; every entry point whose
+// kernels read it (cn_create, cn_debug_disc_quad) uploads it first
+static hipError_t circ_table_init()
+{
+    double cs[64], sn[64];
+    for (int k = 0; k < 64; ++k) { const double a = -(k * (CN_PI / 2 / 16)); cs[k] = cos(a); sn[k] = sin(a); }
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_circ_cos), cs, sizeof cs);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_circ_sin), sn, sizeof sn);
+    return e;
+}
+
 static thread_local char g_err[512];
 static int set_err(int code, const char *fmt, const char *a = "")
 {
@@ -3029,11 +3050,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         g->pend_blocks = g->plan.kd ? (pb + 7) & ~7 : pb;   // leading: a multiple of 8 (XCD placement)
     }
     cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
-    // unit-circle table of GEOS's 64-gon point buffer (norm zones)
-    double cs[64], sn[64];
-    for (int k = 0; k < 64; ++k) { const double a = -(k * (CN_PI / 2 / 16)); cs[k] = cos(a); sn[k] = sin(a); }
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_circ_cos), cs, sizeof cs) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(c_circ_sin), sn, sizeof sn) != hipSuccess) {
+    if (circ_table_init() != hipSuccess) {
         cn_destroy(g);
         return set_err(CN_EHIP, "hipMemcpyToSymbol failed");
     }
@@ -3275,6 +3292,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.pend.case_size = g->case_size;
     a.ov.row = g->rows; a.ov.NS = g->NS;
     a.pend.ov = a.ov;
+    a.cth_h = cos(g->c.human_fov / 2); a.cth_r = cos(g->c.robot_fov / 2);
     g->pend_all = 0;
     const int grid = blocks + g->pend_blocks;
     const bool phx = g->c.rng_mode == CN_RNG_PHILOX;
@@ -3379,6 +3397,7 @@ int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, cons
                        const double *qx, const double *qy, int32_t *out)
 {
     if (n <= 0 || !px || !py || !r || !qx || !qy || !out) return set_err(CN_EINVAL, "cn_debug_disc_quad: n > 0 and buffers required");
+    HIPCHK(circ_table_init());
     hipLaunchKernelGGL(cn_disc_quad_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, n, mode,
                        px, py, r, qx, qy, out);
     HIPCHK(hipGetLastError());

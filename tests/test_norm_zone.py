@@ -58,6 +58,27 @@ def _cases(n=60000, seed=0):
     return px, py, r, qx, qy
 
 
+def _zone_cases(n=40000, seed=1):
+    """The norm zones' own geometry (crowd_sim.py norm-zone penalty; cn_engine.hip:norm_zone): a rectangle
+    whose corner sits ON the robot's circle at the heading (perturbed radially by up to +-1e-3 r, and
+    exactly on it for a quarter of the cases), extending sideways (either side, width 3 r) and forwards
+    (1.8 m) -- the configuration where the 64-gon's vertices decide the answer."""
+    rng = np.random.RandomState(seed)
+    r = rng.uniform(0.2, 0.5, n)
+    px, py = rng.uniform(-5, 5, n), rng.uniform(-5, 5, n)
+    h = rng.uniform(-np.pi, np.pi, n)
+    eps = rng.uniform(-1e-3, 1e-3, n) * r
+    eps[: n // 4] = 0.0
+    cx, cy = px + (r + eps) * np.cos(h), py + (r + eps) * np.sin(h)
+    side = np.where(rng.rand(n) < 0.5, 1.0, -1.0)
+    tx, ty = -np.sin(h) * side, np.cos(h) * side        # tangent (either side)
+    fx, fy = np.cos(h), np.sin(h)                       # forward
+    w, ln = 3 * r, 1.8
+    qx = np.stack([cx, cx + w * tx, cx + w * tx + ln * fx, cx + ln * fx], 1)
+    qy = np.stack([cy, cy + w * ty, cy + w * ty + ln * fy, cy + ln * fy], 1)
+    return px, py, r, qx, qy
+
+
 def test_oracle_known_answers():
     sq_x = np.array([[1.0, 1.0, -1.0, -1.0]])
     sq_y = np.array([[-1.0, 1.0, 1.0, -1.0]])
@@ -78,7 +99,8 @@ def test_gpu_predicate_equals_oracle():
 
     from crowdnav_dsrnn_amd import _lib
 
-    px, py, r, qx, qy = _cases()
+    a, b = _cases(), _zone_cases()
+    px, py, r, qx, qy = (np.concatenate([u, v]) for u, v in zip(a, b))
     want = _oracle(px, py, r, qx, qy)
     dev = torch.device("cuda:0")
     t = [torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(dev) for a in (px, py, r, qx, qy)]
@@ -91,3 +113,5 @@ def test_gpu_predicate_equals_oracle():
         bad = np.nonzero(got != want)[0]
         assert len(bad) == 0, (mode, len(bad), bad[:5])
     assert 0.2 < want.mean() < 0.8   # both outcomes well represented
+    zw = _oracle(*_zone_cases())
+    assert 0.05 < zw.mean() < 0.95, zw.mean()   # the corner-on-circle cases split both ways too
