@@ -708,7 +708,8 @@ struct PendPtrs {
     int32_t *sc;    // [E] scenario
     int64_t *cc;    // [E] key: case_counter the spawn was drawn for
     int32_t *rc;    // [E] key: reset_count (sequential scenario mode)
-    uint32_t *ok;   // [E] entry written
+    uint32_t *ok;   // [E] 0, or the id of the launch that completed the entry (consumed only by a LATER launch)
+    int32_t *prog;  // [E] humans placed so far by a spawn parked mid-way (resumable spawns)
     double *r;      // [5][E] robot px, py, gx, gy, theta
     double *h;      // [7][E*N] human px, py, gx, gy, radius, v_pref, theta
 };
@@ -716,7 +717,7 @@ __host__ __device__ inline PendPtrs pend_slot(const PendPtrs &P, int s, int64_t 
 {
     PendPtrs q = P;
     q.mt += s * E * CN_MT_N; q.pos += s * E; q.ovf += s * E; q.sc += s * E; q.cc += s * E; q.rc += s * E;
-    q.ok += s * E; q.r += s * 5 * E; q.h += s * 7 * EN;
+    q.ok += s * E; q.prog += s * E; q.r += s * 5 * E; q.h += s * 7 * EN;
     return q;
 }
 
@@ -1225,12 +1226,20 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
 // crowd_sim.py:555-663; generate_circle_crossing_human :359-393): reseed the env's stream with
 // counter_offset + case_counter + thisSeed, draw the robot and then each human with rejection.
 // One wave; the result is left in `en` (LDS), rth, ovf, sc and the stream `m`.
+// Resumable (spare-workgroup spawns): i0 > 0 continues a spawn parked after its first i0 humans -- the
+// caller restored the stream, the robot, rth, ovf, sc and those humans -- and with a `deadline` (clock64
+// value, 0 = none) the spawn parks itself before a human once the deadline has passed (at least one
+// human per call). Returns the number of humans placed (N = complete).
 template <bool GRID>
-__device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int64_t case_counter, int32_t reset_count,
-                          int64_t counter_offset, WRng &m, Env1 &en, double &rth, uint32_t &ovf, int &sc)
+__device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64_t case_counter, int32_t reset_count,
+                          int64_t counter_offset, WRng &m, Env1 &en, double &rth, uint32_t &ovf, int &sc,
+                          int i0 = 0, long long deadline = 0)
 {
     const int lane = m.lane;
     const int N = c.human_num;
+    const double R = c.circle_radius;
+    const int W0 = i0;
+    if (i0 == 0) {
     uint32_t *mtw = m.w;
     m.off = 0;   // a fresh stream: the key at the start of the ring
     if (c.scenario_mode == CN_SCMODE_SEQUENTIAL) sc = c.scenarios[reset_count % c.num_scenarios];
@@ -1253,7 +1262,6 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
     wsync();
     m.have1 = false; m.slid = false;
     ovf = 0;
-    const double R = c.circle_radius;
     en.rr = c.robot_radius;
     if (c.kinematics == CN_UNICYCLE) {
         const double angle = m.unif(0, CN_PI * 2);
@@ -1277,8 +1285,10 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
         wsync();
         rth = CN_PI / 2;
     }
+    }   // i0 == 0
     const int W = cand_words(sc);
-    for (int i = 0; i < N; ++i) {
+    for (int i = i0; i < N; ++i) {
+        if (deadline && i > W0 && (long long)clock64() > deadline) return i;   // park (wave-uniform clock)
         double vpref = c.human_vpref, rad = c.human_radius;
         if (c.randomize_attributes) { vpref = m.unif(0.5, 1.5); rad = m.unif(0.3, 0.5); }
         // candidate vs the robot and the humans placed so far (crowd_sim.py:369-390): i + 1 agent tests
@@ -1302,11 +1312,15 @@ __device__ __forceinline__ void spawn_env(const cn_config &c, int64_t gidx, int6
         }
         wsync();
     }
+    return N;
 }
 
 // Store a drawn spawn as env e's pending episode for the reset with key (cc, rc), slot rc & 1.
+// okv: the completing launch's id, or 0 with `prog` = humans placed for a spawn parked mid-way (the
+// stream at the park point, the robot and the first prog humans are stored; resumed by a later launch).
 __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_config &c, int64_t E, int64_t e, const Env1 &en, double rth,
-                              int sc, uint32_t ovf, const uint32_t *mt_src, int pos, int64_t cc, int32_t rc, int lane)
+                              int sc, uint32_t ovf, const uint32_t *mt_src, int pos, int64_t cc, int32_t rc, int lane,
+                              uint32_t okv, int prog)
 {
     const int N = c.human_num;
     const PendPtrs P = pend_slot(P2, rc & 1, E, E * N);
@@ -1318,7 +1332,7 @@ __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_confi
 #pragma unroll
         for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) { const int k = lane + 64 * j; if (k < nk) P.mt[e * CN_MT_N + k] = v[j]; }
     }
-    if (lane < N) {
+    if (lane < prog) {
         const int64_t h = e * N + lane, EN = E * N;
         P.h[h] = en.hpx[lane]; P.h[EN + h] = en.hpy[lane]; P.h[2 * EN + h] = en.hgx[lane];
         P.h[3 * EN + h] = en.hgy[lane]; P.h[4 * EN + h] = en.hr[lane]; P.h[5 * EN + h] = en.hvp[lane];
@@ -1327,7 +1341,8 @@ __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_confi
     if (lane == 0) {
         P.r[e] = en.rpx; P.r[E + e] = en.rpy; P.r[2 * E + e] = en.rgx; P.r[3 * E + e] = en.rgy; P.r[4 * E + e] = rth;
         P.pos[e] = pos; P.ovf[e] = ovf; P.sc[e] = sc; P.cc[e] = cc; P.rc[e] = rc;
-        P.ok[e] = 1u;
+        P.prog[e] = okv ? 0 : prog;
+        P.ok[e] = okv;
     }
 }
 
@@ -1602,7 +1617,7 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
 // spawn when `may_consume` and it is valid for the current key, else draw it here. One wave.
 template <bool GRID>
 __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2, const cn_config &c, int64_t E, int64_t e,
-                          int64_t counter_offset, bool may_consume, WRng &m, Env1 &en)
+                          int64_t counter_offset, bool may_consume, uint32_t launch_id, WRng &m, Env1 &en)
 {
     const cn_state_ptrs &S = o.s;
     const int N = c.human_num;
@@ -1610,7 +1625,10 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2,
     const int64_t cc = S.case_counter[e];
     const int32_t rc = S.reset_count[e];
     const PendPtrs P = pend_slot(P2, rc & 1, E, E * N);
-    if (may_consume && P.ok[e] && P.cc[e] == cc && P.rc[e] == rc) {
+    // an entry completed by THIS launch (a resumed spawn finishing beside this reset) is not consumed: its
+    // stores need not be visible yet; the reset draws inline instead
+    const uint32_t ok = P.ok[e];
+    if (may_consume && ok && ok != launch_id && P.cc[e] == cc && P.rc[e] == rc) {
         if (lane < N) {
             const int64_t h = e * N + lane, EN = E * N;
             double v[7];
@@ -1641,6 +1659,10 @@ struct PendLaunch {
     PendPtrs P;
     const uint32_t *list;   // envs reset by the previous launch
     const uint32_t *count;
+    const uint32_t *rlist;  // spawns parked by the previous launch: {e | 2^31 if not started, key rc, cc lo, cc hi}
+    const uint32_t *rcount;
+    uint32_t *rlist_w;      // spawns this launch parks
+    uint32_t *rcount_w;
     int all;                // 1: every env (list ignored)
     int step_blocks, pend_blocks;
     int first;              // 1: workgroups [0, pend_blocks) (kd-tree path); 0: after the step workgroups
@@ -1649,24 +1671,62 @@ struct PendLaunch {
     int64_t counter_offset;
     int64_t case_size;
     OutView ov;             // global env index = c.env_offset + orow(ov, e)
+    long long budget;       // clock cycles a spawning wave works before parking (0: never parks)
+    uint32_t launch_id;     // nonzero id of this launch (pending entries it completes carry it)
 };
 
-// GRID: the spawn's crowded rejection through a DiscGrid (the kd-tree path's plans have LDS for it)
+// GRID: the spawn's crowded rejection through a DiscGrid (the kd-tree path's plans have LDS for it).
+// Items: the envs reset by the previous launch (their spawn for the reset after next), then the spawns
+// the previous launch parked. With a budget, a wave parks its spawn between two humans once the budget
+// is spent (stream, robot and humans so far go to the pending slot, the item to rlist_w) and parks the
+// items it has not started; a later launch resumes them. The pending slot of a spawn is written only by
+// the wave that owns the item, and a reset consumes an entry only if an EARLIER launch completed it.
 template <bool PHX, bool GRID>
 __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_ptrs &S, const cn_config &c, int E, char *smem)
 {
     const int nw = pl.waves, w = threadIdx.x / 64, lane = threadIdx.x & 63;
     if (w >= nw) return;
+    const int N = c.human_num;
     char *base = smem + w * pl.stride;
     uint32_t *mtw = (uint32_t *)base;
     double *hb = (double *)(base + 2 * CN_MT_N * 4);
     // envs reset by the previous launch: the reset after next (the next one was drawn earlier); after
     // cn_reset / cn_set_state (all): both the next (items [0, E)) and the one after ([E, 2E))
-    const uint32_t n = pl.all ? (uint32_t)(2 * E) : min(*pl.count, (uint32_t)E);
+    const uint32_t nnew = pl.all ? (uint32_t)(2 * E) : min(*pl.count, (uint32_t)E);
+    // parking / resuming exists on the kd-tree path only (GRID): the quad path's spawns are short, and
+    // its kernel keeps the plain loop (register pressure of the step path)
+    const uint32_t nres = (!GRID || pl.all) ? 0u : min(*pl.rcount, (uint32_t)(2 * E));
     const int pb = pl.first ? (int)blockIdx.x : (int)blockIdx.x - pl.step_blocks;
-    for (uint32_t it = (uint32_t)(pb * nw + w); it < n; it += (uint32_t)(pl.pend_blocks * nw)) {
-        const int64_t e = pl.all ? (int64_t)(it % (uint32_t)E) : (int64_t)pl.list[it];
-        const bool ahead2 = !pl.all || it >= (uint32_t)E;
+    const long long deadline = (GRID && pl.budget) ? (long long)clock64() + pl.budget : 0;
+    for (uint32_t it = (uint32_t)(pb * nw + w); it < nnew + nres; it += (uint32_t)(pl.pend_blocks * nw)) {
+        int64_t e, cc;
+        int32_t rc;
+        bool started = false;
+        if (it < nnew) {
+            e = pl.all ? (int64_t)(it % (uint32_t)E) : (int64_t)pl.list[it];
+            const bool ahead2 = !pl.all || it >= (uint32_t)E;
+            cc = S.case_counter[e];
+            rc = S.reset_count[e];
+            if (ahead2) { cc = (cc + c.nenv) % pl.case_size; rc += 1; }   // write_reset's counter update
+        } else {
+            const uint32_t *q = pl.rlist + 4 * (it - nnew);
+            e = (int64_t)(q[0] & 0x7fffffffu);
+            started = (q[0] >> 31) == 0u;
+            rc = (int32_t)q[1];
+            cc = (int64_t)((uint64_t)q[2] | ((uint64_t)q[3] << 32));
+            if (rc < S.reset_count[e]) continue;   // its reset has come and gone (drawn inline)
+        }
+        if (deadline && (long long)clock64() > deadline) {   // out of budget: park the item unstarted / as is
+            if (lane == 0) {
+                const uint32_t k = atomicAdd(pl.rcount_w, 1u);
+                if (k < (uint32_t)(2 * E)) {
+                    uint32_t *q = pl.rlist_w + 4 * k;
+                    q[0] = (uint32_t)e | (started ? 0u : 0x80000000u); q[1] = (uint32_t)rc;
+                    q[2] = (uint32_t)(uint64_t)cc; q[3] = (uint32_t)((uint64_t)cc >> 32);
+                }
+            }
+            continue;
+        }
         Env1 en;
         en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
         en.hth = hb + 192;
@@ -1674,21 +1734,46 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         m.w = mtw; m.off = 0; m.lane = lane; m.phx = PHX; m.edbg = -1;
         m.grid = pl.stride > CN_PEND_LDS ? base + CN_PEND_LDS : nullptr;
         m.sl = (double *)(base + 2 * CN_MT_N * 4 + 7 * 32 * 8);
-        int64_t cc = S.case_counter[e];
-        int32_t rc = S.reset_count[e];
-        if (ahead2) { cc = (cc + c.nenv) % pl.case_size; rc += 1; }   // write_reset's counter update
-        double rth;
-        uint32_t ovf;
-        int sc;
+        double rth = 0;
+        uint32_t ovf = 0;
+        int sc = 0, i0 = 0;
+        if (GRID && started) {   // restore the parked spawn: stream at the park point, robot, the humans so far
+            const PendPtrs P = pend_slot(pl.P, rc & 1, E, (int64_t)E * N);
+            i0 = P.prog[e];
+            const int nk = PHX ? 1 : CN_MT_N;
+            for (int k = lane; k < nk; k += 64) mtw[k] = P.mt[e * CN_MT_N + k];
+            if (lane < i0) {
+                const int64_t h = e * N + lane, EN = (int64_t)E * N;
+                en.hpx[lane] = P.h[h]; en.hpy[lane] = P.h[EN + h]; en.hgx[lane] = P.h[2 * EN + h];
+                en.hgy[lane] = P.h[3 * EN + h]; en.hr[lane] = P.h[4 * EN + h]; en.hvp[lane] = P.h[5 * EN + h];
+                en.hth[lane] = P.h[6 * EN + h];
+            }
+            en.rpx = P.r[e]; en.rpy = P.r[E + e]; en.rgx = P.r[2 * E + e]; en.rgy = P.r[3 * E + e];
+            rth = P.r[4 * E + e];
+            en.rr = c.robot_radius;
+            ovf = P.ovf[e]; sc = P.sc[e];
+            m.p = P.pos[e]; m.have1 = false; m.slid = false;
+            m.key = mtw[0];
+            wsync();
+        }
 #ifdef CN_STAMPS
         const unsigned long long ts0 = clock64();
 #endif
-        spawn_env<GRID>(c, c.env_offset + orow(pl.ov, e), cc, rc, pl.counter_offset, m, en, rth, ovf, sc);
+        const int done = spawn_env<GRID>(c, c.env_offset + orow(pl.ov, e), cc, rc, pl.counter_offset, m, en, rth, ovf,
+                                         sc, i0, deadline);
         const bool in1 = !m.phx && m.p > CN_MT_N;
         write_pending(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
-                      lane);
+                      lane, done == N ? pl.launch_id : 0u, done);
+        if (GRID && done < N && lane == 0) {   // parked mid-way
+            const uint32_t k = atomicAdd(pl.rcount_w, 1u);
+            if (k < (uint32_t)(2 * E)) {
+                uint32_t *q = pl.rlist_w + 4 * k;
+                q[0] = (uint32_t)e; q[1] = (uint32_t)rc;
+                q[2] = (uint32_t)(uint64_t)cc; q[3] = (uint32_t)((uint64_t)cc >> 32);
+            }
+        }
 #ifdef CN_STAMPS
-        if (lane == 0 && e < 8192) { cn_stamp_p[2 * e] = ts0; cn_stamp_p[2 * e + 1] = clock64(); }
+        if (lane == 0 && e < 8192 && done == N) { cn_stamp_p[2 * e] = ts0; cn_stamp_p[2 * e + 1] = clock64(); }
 #endif
         wsync();
     }
@@ -1710,6 +1795,7 @@ struct StepArgs {
     uint32_t *plist_w;      // envs reset by this launch (their next spawn is drawn by the next launch)
     uint32_t *pcount_w;
     uint32_t *pcount_zero;  // the counter the NEXT launch appends to (triple-buffered), zeroed here
+    uint32_t *rcount_zero;  // likewise for the parked-spawn list
     PendLaunch pend;        // spawn waves: the first or the last pend_blocks workgroups (pend.first)
     int64_t case_size;
     int E;
@@ -1758,7 +1844,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const OutView ov = MIX ? g.ov : OutView{nullptr, c.human_num};
     // the spawn-list counter the NEXT launch appends to (neither read nor appended to by this launch)
-    if (blockIdx.x == 0 && threadIdx.x == 0) *g.pcount_zero = 0u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { *g.pcount_zero = 0u; *g.rcount_zero = 0u; }
     const int sb = (int)blockIdx.x - (g.pend.first ? g.pend.pend_blocks : 0);   // step workgroup index
     if (sb < 0 || sb >= g.pend.step_blocks) {  // spare workgroups: draw upcoming episodes' spawns
         PendLaunch pl = g.pend;
@@ -2528,7 +2614,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
                 const bool may = !g.pend.all;   // both pending slots are ready unless this launch draws all
-                reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, m, en);
+                reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m, en);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
                     const uint32_t k = atomicAdd(g.pcount_w, 1u);
                     if (k < (uint32_t)g.E) g.plist_w[k] = (uint32_t)e;
@@ -2569,7 +2655,7 @@ __global__ void __launch_bounds__(64) cn_reset_kernel(RngArgs g, cn_config c)
         WRng m;
         m.w = mtw; m.off = 0; m.lane = lane; m.sl = slots; m.phx = c.rng_mode == CN_RNG_PHILOX; m.edbg = -1;
         m.grid = gridbuf;
-        reset_env<true>(g.o, g.pend, c, g.E, e, g.counter_offset, true, m, en);
+        reset_env<true>(g.o, g.pend, c, g.E, e, g.counter_offset, true, 0u, m, en);
     }
 }
 
@@ -2788,6 +2874,8 @@ struct cn_engine {
     uint32_t *work;       // [E]
     uint32_t *work_count; // [16]: [2..4] spawn-list counters (triple buffered)
     uint32_t *plist;      // [3][E] envs whose next spawn kernel A draws
+    uint32_t *rlist;      // [3][2E][4] spawns parked by a launch (resumed by the next); counters work_count[5..7]
+    long long spawn_budget;   // clock cycles a spawning wave works per launch before parking (0: never)
     void *pend_mem;       // pending next-episode spawns (PendPtrs)
     PendPtrs pend;
     int pend_all;         // next kernel A draws every env's spawn (after cn_reset / cn_set_state)
@@ -3006,14 +3094,17 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     // pending spawns: every array holds both slots ([2][...], pend_slot)
     const int64_t pb_mt = al(2 * E * CN_MT_N * 4), pb_i = al(2 * E * 4), pb_cc = al(2 * E * 8), pb_r = al(2 * 5 * E * 8),
                   pb_h = al(2 * 7 * EN * 8);
-    const int64_t pend_bytes = pb_mt + 5 * pb_i + pb_cc + pb_r + pb_h;
+    const int64_t pend_bytes = pb_mt + 6 * pb_i + pb_cc + pb_r + pb_h;
     hipError_t e1 = hipMalloc(&g->state, g->state_bytes);
     hipError_t e2 = hipMalloc(&g->work, sizeof(uint32_t) * (g->E + 64));
     hipError_t e3 = hipMalloc(&g->work_count, 64);
     hipError_t e4 = hipMalloc(&g->plist, sizeof(uint32_t) * 3 * (g->E + 64));
+    hipError_t e6 = hipMalloc(&g->rlist, sizeof(uint32_t) * 3 * 4 * (2 * (int64_t)g->E + 64));
     hipError_t e5 = hipMalloc(&g->pend_mem, pend_bytes);
-    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess) {
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess ||
+        e6 != hipSuccess) {
         (void)hipFree(g->state); (void)hipFree(g->work); (void)hipFree(g->work_count); (void)hipFree(g->plist); (void)hipFree(g->pend_mem);
+        (void)hipFree(g->rlist);
         delete g;
         return set_err(CN_ENOMEM, "hipMalloc failed");
     }
@@ -3030,6 +3121,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         g->pend.sc = (int32_t *)b; b += pb_i;
         g->pend.rc = (int32_t *)b; b += pb_i;
         g->pend.ok = (uint32_t *)b; b += pb_i;
+        g->pend.prog = (int32_t *)b; b += pb_i;
         g->pend.cc = (int64_t *)b; b += pb_cc;
         g->pend.r = (double *)b; b += pb_r;
         g->pend.h = (double *)b;
@@ -3048,6 +3140,10 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         const int cap = (g->plan.kd ? 256 : 128) / nw;
         const int pb = (int)(need < cap ? need : cap);
         g->pend_blocks = g->plan.kd ? (pb + 7) & ~7 : pb;   // leading: a multiple of 8 (XCD placement)
+        // kd-tree path: a crowded spawn (~1M cycles) may take longer than the launch's step rounds; each
+        // spawning wave parks its spawn after ~0.6M cycles and a later launch resumes it (the spawn is
+        // needed one whole episode later). The quad path's spawns are short: never parked.
+        g->spawn_budget = g->plan.kd ? 600000 : 0;
     }
     cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
     if (circ_table_init() != hipSuccess) {
@@ -3224,6 +3320,7 @@ void cn_destroy(cn_engine *g)
     (void)hipFree(g->work);
     (void)hipFree(g->work_count);
     (void)hipFree(g->plist);
+    (void)hipFree(g->rlist);
     (void)hipFree(g->pend_mem);
     delete g;
 }
@@ -3282,6 +3379,11 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.plist_w = g->plist + (int64_t)kw * (g->E + 64);
     a.pcount_w = g->work_count + 2 + kw;
     a.pcount_zero = g->work_count + 2 + kz;
+    a.rcount_zero = g->work_count + 5 + kz;
+    a.pend.rlist = g->rlist + (int64_t)kr * 4 * (2 * (int64_t)g->E + 64); a.pend.rcount = g->work_count + 5 + kr;
+    a.pend.rlist_w = g->rlist + (int64_t)kw * 4 * (2 * (int64_t)g->E + 64); a.pend.rcount_w = g->work_count + 5 + kw;
+    a.pend.budget = g->spawn_budget;
+    a.pend.launch_id = (uint32_t)(g->nstep % 0x7ffffffeu) + 1u;   // nonzero, differs from the neighbours'
     const int blocks = (g->E + g->plan.EPB - 1) / g->plan.EPB;
     a.pend.P = g->pend; a.pend.list = g->plist + (int64_t)kr * (g->E + 64); a.pend.count = g->work_count + 2 + kr;
     a.pend.all = g->pend_all;
