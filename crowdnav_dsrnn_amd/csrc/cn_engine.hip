@@ -1905,17 +1905,27 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     uint32_t pre_dm = 0u;
     int32_t pre_epl = 0, pre_sc = 0;
     uint32_t pre_ovf = 0;
+    // With a 360-degree robot FOV every human the robot can see is visible (only coincident agents are
+    // not), so the previous belief is read only in that rare case, straight from the state in phase 4
+    const bool rfull = c.robot_fov >= 2.0 * CN_PI;
     if (hl) {
         // every load issued before the first LDS store (the compiler otherwise waits on each load in turn)
         double hv[CN_HUM_F];
         pre_or = S.o_r[gh]; pre_vmax = S.o_vmax[gh]; pre_dm = S.o_dmask[gh];
         hv[H_PX] = S.h_px[gh]; hv[H_PY] = S.h_py[gh]; hv[H_GX] = S.h_gx[gh]; hv[H_GY] = S.h_gy[gh];
         hv[H_VX] = S.h_vx[gh]; hv[H_VY] = S.h_vy[gh]; hv[H_R] = S.h_r[gh]; hv[H_VP] = S.h_vpref[gh];
-        hv[H_TH] = S.h_theta[gh]; hv[H_BPX] = S.b_px[gh]; hv[H_BPY] = S.b_py[gh]; hv[H_BVX] = S.b_vx[gh];
-        hv[H_BVY] = S.b_vy[gh]; hv[H_BR] = S.b_r[gh];
+        hv[H_TH] = S.h_theta[gh];
+        if (!rfull) {
+            hv[H_BPX] = S.b_px[gh]; hv[H_BPY] = S.b_py[gh]; hv[H_BVX] = S.b_vx[gh]; hv[H_BVY] = S.b_vy[gh];
+            hv[H_BR] = S.b_r[gh];
+        }
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int f = 0; f < CN_HUM_F; ++f) HF(sl, f, tid) = hv[f];
+        for (int f = 0; f < H_BPX; ++f) HF(sl, f, tid) = hv[f];
+        if (!rfull) {
+#pragma unroll
+            for (int f = H_BPX; f < CN_HUM_F; ++f) HF(sl, f, tid) = hv[f];
+        }
     }
     STAMP_A(12);
     if (rl) {
@@ -2524,8 +2534,13 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         if (rv) {
             bpx = npx; bpy = npy; bvx = nvx; bvy = nvy; br = HF(sl, H_R, tid);
         } else {
-            bvx = HF(sl, H_BVX, tid); bvy = HF(sl, H_BVY, tid); br = HF(sl, H_BR, tid);
-            bpx = HF(sl, H_BPX, tid) + bvx * dt; bpy = HF(sl, H_BPY, tid) + bvy * dt;
+            if (rfull) {   // coincident with the robot (or a NaN state): the stored belief, extrapolated
+                bvx = S.b_vx[gh]; bvy = S.b_vy[gh]; br = S.b_r[gh];
+                bpx = S.b_px[gh] + bvx * dt; bpy = S.b_py[gh] + bvy * dt;
+            } else {
+                bvx = HF(sl, H_BVX, tid); bvy = HF(sl, H_BVY, tid); br = HF(sl, H_BR, tid);
+                bpx = HF(sl, H_BPX, tid) + bvx * dt; bpy = HF(sl, H_BPY, tid) + bvy * dt;
+            }
         }
         S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = bvx; S.b_vy[gh] = bvy; S.b_r[gh] = br;
         const int64_t oh = orow(ov, e0 + el) * ov.NS + i;
