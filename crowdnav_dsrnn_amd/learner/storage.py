@@ -4,11 +4,53 @@ API and semantics as the reference: obs / recurrent_hidden_states dicts of (T+1,
 insert(), after_update(), compute_returns() (all four GAE / proper-time-limit branches, :132-177) and the
 two minibatch generators. compact_hidden=True keeps 2 hidden-state slots instead of T+1
 (slot 0 = rollout start, read by the recurrent generator; slot 1 = latest, carried by after_update): 96 MB
-instead of 6.2 GB at 4096 envs x 128 steps; read the step's state with hidden(step). The generators gather with index tensors instead of per-env Python loops; the
+instead of 6.2 GB at 4096 envs x 128 steps. Its recurrent_hidden_states still index like the reference's
+(T+1)-step tensors (CompactSteps): [0] is the rollout start, any other step the latest state -- what
+train.py reads at [step] before act() and at [-1] for the next value -- so train.py runs unmodified.
+The generators gather with index tensors instead of per-env Python loops; the
 environment permutation is drawn with torch.randperm on the default CPU generator exactly as the
 reference does (:231), so a seeded run produces the same minibatches.
 """
 import torch
+
+
+class CompactSteps:
+    """A (2, ...) hidden-state tensor indexed as the (T+1, ...) one it replaces: integer index 0 (or
+    -(T+1)) is slot 0 (the rollout start), every other step is slot 1 (the latest state, the only one a
+    rollout reads after step 0); slices and every tensor attribute go to the 2-slot tensor itself."""
+
+    def __init__(self, t, T):
+        self.t, self.T = t, T
+
+    def _slot(self, i):
+        i = int(i)
+        if not -(self.T + 1) <= i <= self.T:
+            raise IndexError("step %d out of range for %d steps" % (i, self.T))
+        return 0 if i in (0, -(self.T + 1)) else 1
+
+    def __getitem__(self, i):
+        if isinstance(i, int) or (hasattr(i, "__index__") and not isinstance(i, (slice, torch.Tensor))):
+            return self.t[self._slot(i)]
+        return self.t[i]
+
+    def __setitem__(self, i, v):
+        if isinstance(i, int):
+            self.t[self._slot(i)] = v
+        else:
+            self.t[i] = v
+
+    def __len__(self):
+        return self.T + 1
+
+    def to(self, *a, **kw):
+        return CompactSteps(self.t.to(*a, **kw), self.T)
+
+    def __getattr__(self, n):
+        return getattr(self.t, n)
+
+
+def _raw(v):
+    return v.t if isinstance(v, CompactSteps) else v
 
 
 def _flatten_helper(T, N, x):
@@ -32,6 +74,8 @@ class SRNNRolloutStorage:
             "human_human_edge_rnn": torch.zeros(TH, E, self.human_num + 1, human_human_edge_rnn_size * dbl,
                                                 device=dev),
         }
+        if self.compact_hidden:
+            self.recurrent_hidden_states = {k: CompactSteps(v, T) for k, v in self.recurrent_hidden_states.items()}
         self.rewards = torch.zeros(T, E, 1, device=dev)
         self.value_preds = torch.zeros(T + 1, E, 1, device=dev)
         self.returns = torch.zeros(T + 1, E, 1, device=dev)
@@ -57,9 +101,8 @@ class SRNNRolloutStorage:
         s = self.step
         for k in self.obs:
             self.obs[k][s + 1].copy_(obs[k])
-        hs = 1 if self.compact_hidden else s + 1
         for k in recurrent_hidden_states:
-            dst = self.recurrent_hidden_states[k][hs]
+            dst = self.recurrent_hidden_states[k][s + 1]
             if recurrent_hidden_states[k].data_ptr() != dst.data_ptr():   # act(out_hxs=hidden_slot()) wrote it
                 dst.copy_(recurrent_hidden_states[k])
         self.actions[s].copy_(actions)
@@ -72,13 +115,11 @@ class SRNNRolloutStorage:
 
     def hidden(self, step):
         """The recurrent state act() consumes at `step` (recurrent_hidden_states[k][step] in train.py:227)."""
-        i = (0 if step == 0 else 1) if self.compact_hidden else step
-        return {k: v[i] for k, v in self.recurrent_hidden_states.items()}
+        return {k: v[step] for k, v in self.recurrent_hidden_states.items()}
 
     def hidden_slot(self):
         """Where insert() puts the state produced at the current step (act's out_hxs target)."""
-        i = 1 if self.compact_hidden else self.step + 1
-        return {k: v[i] for k, v in self.recurrent_hidden_states.items()}
+        return {k: v[self.step + 1] for k, v in self.recurrent_hidden_states.items()}
 
     def after_update(self):
         for d in (self.obs, self.recurrent_hidden_states):
@@ -140,6 +181,8 @@ class SRNNRolloutStorage:
         for indices in BatchSampler(SubsetRandomSampler(range(batch)), mini_batch_size, drop_last=True):
             idx = torch.as_tensor(indices, device=self.rewards.device)
             obs_b = {k: v[:-1].reshape(-1, *v.shape[2:])[idx] for k, v in self.obs.items()}
+            if self.compact_hidden:
+                raise NotImplementedError("feed_forward_generator needs every step's hidden state (compact_hidden=False)")
             hxs_b = {k: v[:-1].reshape(-1, v.shape[-1])[idx] for k, v in self.recurrent_hidden_states.items()}
             yield (obs_b, hxs_b, self.actions.reshape(-1, self.actions.shape[-1])[idx],
                    self.value_preds[:-1].reshape(-1, 1)[idx], self.returns[:-1].reshape(-1, 1)[idx],
@@ -161,6 +204,8 @@ class RolloutStorage(SRNNRolloutStorage):
         TH = 2 if compact_hidden else T + 1
         self.obs = torch.zeros(T + 1, E, *tuple(obs_shape), device=dev)
         self.recurrent_hidden_states = torch.zeros(TH, E, recurrent_hidden_state_size, device=dev)
+        if self.compact_hidden:
+            self.recurrent_hidden_states = CompactSteps(self.recurrent_hidden_states, T)
         self.rewards = torch.zeros(T, E, 1, device=dev)
         self.value_preds = torch.zeros(T + 1, E, 1, device=dev)
         self.returns = torch.zeros(T + 1, E, 1, device=dev)
@@ -183,7 +228,7 @@ class RolloutStorage(SRNNRolloutStorage):
                bad_masks):
         s = self.step
         self.obs[s + 1].copy_(obs)
-        self.recurrent_hidden_states[1 if self.compact_hidden else s + 1].copy_(recurrent_hidden_states)
+        self.recurrent_hidden_states[s + 1].copy_(recurrent_hidden_states)
         self.actions[s].copy_(actions)
         self.action_log_probs[s].copy_(action_log_probs)
         self.value_preds[s].copy_(value_preds)
@@ -193,7 +238,7 @@ class RolloutStorage(SRNNRolloutStorage):
         self.step = (s + 1) % self.num_steps
 
     def hidden(self, step):
-        return self.recurrent_hidden_states[(0 if step == 0 else 1) if self.compact_hidden else step]
+        return self.recurrent_hidden_states[step]
 
     def after_update(self):
         self.obs[0].copy_(self.obs[-1])
@@ -228,6 +273,8 @@ class RolloutStorage(SRNNRolloutStorage):
         if mini_batch_size is None:
             assert batch >= num_mini_batch
             mini_batch_size = batch // num_mini_batch
+        if self.compact_hidden:
+            raise NotImplementedError("feed_forward_generator needs every step's hidden state (compact_hidden=False)")
         for indices in BatchSampler(SubsetRandomSampler(range(batch)), mini_batch_size, drop_last=True):
             idx = torch.as_tensor(indices, device=self.rewards.device)
             yield (self.obs[:-1].reshape(-1, *self.obs.shape[2:])[idx],

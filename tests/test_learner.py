@@ -90,6 +90,35 @@ def test_compact_hidden_same_minibatches(fx):
         assert torch.equal(full.recurrent_hidden_states[k][0], comp.recurrent_hidden_states[k][0])
 
 
+def test_compact_hidden_reference_indexing():
+    """train.py:232-236,298-302 index the storage as (T+1)-step tensors -- [key][step] before act() and
+    [key][-1] for the next value -- and insert the new state at step + 1: with compact_hidden the same
+    code reads the same states as with the full buffer."""
+    from crowdnav_dsrnn_amd import spaces
+
+    obs_sp, act_sp = spaces.observation_space(N).spaces, spaces.action_space()
+    full = SRNNRolloutStorage(T, E, obs_sp, act_sp, 128, 256, "GRU", device="cpu")
+    comp = SRNNRolloutStorage(T, E, obs_sp, act_sp, 128, 256, "GRU", device="cpu", compact_hidden=True)
+    g = torch.Generator().manual_seed(5)
+    for rol in (full, comp):
+        for k, v in rol.recurrent_hidden_states.items():
+            v[0].copy_(torch.randn(v[0].shape, generator=torch.Generator().manual_seed(1)))
+    for step in range(T):
+        h_full = {k: full.recurrent_hidden_states[k][step] for k in full.recurrent_hidden_states}
+        h_comp = {k: comp.recurrent_hidden_states[k][step] for k in comp.recurrent_hidden_states}
+        for k in h_full:
+            assert torch.equal(h_full[k], h_comp[k]), (step, k)
+        new = {k: torch.randn(v.shape, generator=g) for k, v in h_full.items()}
+        obs = {k: torch.zeros(v.shape[1:]) for k, v in full.obs.items()}
+        args = (obs, new, torch.zeros(E, 2), torch.zeros(E, 1), torch.zeros(E, 1), torch.zeros(E, 1),
+                torch.ones(E, 1), torch.ones(E, 1))
+        full.insert(*args)
+        comp.insert(*args)
+    for k in full.recurrent_hidden_states:
+        assert torch.equal(full.recurrent_hidden_states[k][-1], comp.recurrent_hidden_states[k][-1])
+        assert len(comp.recurrent_hidden_states[k]) == T + 1
+
+
 def _update(fx, device):
     pol = make_policy(N, E=E, T=T, device=device)
     pol.base.nminibatch = 2
