@@ -257,3 +257,48 @@ def test_gpu_full_size_c2_free_running(gpu, oracle):
     assert n_ep[1] > 1000, n_ep
     assert abs(n_ep[1] - n_ep[0]) <= 0.02 * n_ep[0], n_ep
     assert abs(ret[1] / n_ep[1] - ret[0] / n_ep[0]) <= 0.02 * abs(ret[0] / n_ep[0]) + 0.05, (ret, n_ep)
+
+
+@pytest.mark.parametrize("E,N,kin,scen,fov", [
+    (4099, 10, "unicycle", "circle_crossing", 2.0),    # ragged: E not a multiple of the 6 envs per workgroup
+    (1, 10, "unicycle", "circle_crossing", 2.0),       # a single env (one partly filled workgroup)
+    (203, 25, "holonomic", "square_crossing", 1.0),    # ragged on the kd-tree path (2 envs per workgroup)
+])
+def test_gpu_ragged_sizes_match_oracle(gpu, oracle, E, N, kin, scen, fov):
+    """Free-running GPU == oracle for 30 steps at batch sizes that leave the last workgroup partly empty."""
+    cfg = _cfg(N, kin, scen, E=E, fov=fov)
+    ref, g = oracle.RefEngine(cfg), gpu(cfg)
+    o1, o2 = ref.reset(), g.reset()
+    for k in o1:
+        np.testing.assert_allclose(o2[k], o1[k], atol=1e-6, rtol=0)
+    rng = np.random.RandomState(13)
+    for t in range(30):
+        a = (rng.uniform(-0.1, 0.1, (E, 2)) if kin == "unicycle" else rng.normal(0, 0.5, (E, 2))).astype(np.float32)
+        r1, r2 = ref.step(a), g.step(a)
+        np.testing.assert_array_equal(r2[2], r1[2], err_msg="done t=%d" % t)
+        np.testing.assert_array_equal(r2[3], r1[3], err_msg="event t=%d" % t)
+        np.testing.assert_allclose(r2[1], r1[1], atol=1e-5, rtol=0, err_msg="reward t=%d" % t)
+        for k in r1[0]:
+            np.testing.assert_allclose(r2[0][k], r1[0][k], atol=1e-5, rtol=0, err_msg="%s t=%d" % (k, t))
+
+
+def test_gpu_large_batch_properties(gpu):
+    """A large batch (131,072 envs x 10 humans, 32x the bench's: 21,846 workgroups, spawn lists of
+    thousands of entries) for 40 steps: finite outputs, done exactly on terminal events, Monitor lengths
+    positive where done, every env's stream position advanced consistently with its resets."""
+    E = 131072
+    cfg = _cfg(10, "unicycle", E=E)
+    g = gpu(cfg)
+    g.reset()
+    rng = np.random.RandomState(1)
+    term = np.isin(np.arange(5), [abi.EV_COLLISION, abi.EV_REACHGOAL, abi.EV_TIMEOUT])
+    resets = np.zeros(E, np.int64)
+    for t in range(40):
+        r = g.step(rng.uniform(-0.1, 0.1, (E, 2)).astype(np.float32))
+        assert np.isfinite(r[1]).all() and all(np.isfinite(v).all() for v in r[0].values()), t
+        d = r[2].astype(bool)
+        np.testing.assert_array_equal(d, term[r[3]], err_msg="t=%d" % t)
+        assert (r[6][d] >= 1).all()
+        resets += d
+    st = g.get_state()
+    np.testing.assert_array_equal(st.reset_count.astype(np.int64), 1 + resets)   # cn_reset + auto-resets
