@@ -496,20 +496,6 @@ __device__ __forceinline__ int quad_or(int x)
     return x | quad_xor2i(x);
 }
 
-// min / max over aligned groups of 8 lanes (quad, then row_half_mirror across the two quads; exact)
-__device__ __forceinline__ float oct_min(float x)
-{
-    x = quad_min(x);
-    const float y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false));
-    return y < x ? y : x;
-}
-__device__ __forceinline__ float oct_max(float x)
-{
-    x = quad_max(x);
-    const float y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false));
-    return x < y ? y : x;
-}
-
 // linearProgram1 on line `no` of Lb (valid lines: bits of vmask), quad-cooperative
 __device__ __forceinline__ bool lp1_q(const float4 *Lb, uint32_t vmask, int no, float radius, int s, float &tL,
                                       float &tR)
@@ -2167,40 +2153,40 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                     STAMP_A(15);
                     // (2) KdTree build (buildAgentTreeRecursive, which re-permutes the persisted agents_ order)
                     //     fused with the query's depth-first walk (queryAgentTreeRecursive: closer child first,
-                    //     ties -> right). 8 lanes per human (lane sub holds positions sub, sub+8, sub+16,
-                    //     sub+24 of the agent order), 8 humans per wave at a time. Every node is partitioned
+                    //     ties -> right). 4 lanes per human (lane sub holds positions sub, sub+4, ..., sub+28
+                    //     of the agent order), all 16 humans of a wave at once (8 lanes and two rounds of 8
+                    //     humans before: the walk's critical path was twice as long). Every node is partitioned
                     //     once: Hoare's two-pointer loop swaps the i-th element >= split left of the cut with the
                     //     i-th element < split counted from the right end, which ballots and popcounts give
                     //     directly (exchange through the human's projected-lines space). The children's
-                    //     bounding boxes (exact min / max over the 8 lanes) give both the visiting order and
+                    //     bounding boxes (exact min / max over the quad) give both the visiting order and
                     //     their own split. Pruned subtrees hold no agent within range, so walking them inserts
                     //     nothing: the in-range agents' visiting order tpos is the order
                     //     Agent::insertAgentNeighbor sees. The explicit stack (<= A - 9 entries) lives in the
                     //     sorted-lines space, written only after the walk.
                     {
-                        const int lane = tid & 63, grp = lane >> 3, sub = lane & 7;
+                        const int lane = tid & 63, grp = lane >> 2, sub = lane & 3;
                         const int wbase = (tid >> 6) * 16;
-                        auto gmask = [&](const bool (&pr)[4]) -> uint32_t {
+                        auto gmask = [&](const bool (&pr)[8]) -> uint32_t {
                             uint32_t m = 0;
 #pragma unroll
-                            for (int u = 0; u < 4; ++u)
-                                m |= (uint32_t)((__ballot(pr[u]) >> (8 * grp)) & 0xffull) << (8 * u);
+                            for (int u = 0; u < 8; ++u)
+                                m |= (uint32_t)((__ballot(pr[u]) >> (4 * grp)) & 0xfull) << (4 * u);
                             return m;
                         };
-                        for (int r = 0; r < 2; ++r) {
-                            const int hw = wbase + grp + 8 * r;
-                            if (hw >= nh) continue;
+                        if (wbase + grp < nh) {   // 16 humans per wave, 4 lanes each, all at once
+                            const int hw = wbase + grp;
                             const int elw = hw / N, iw = hw - elw * N;
                             const int gw = (e0 + elw) * N + iw;
                             const float *Dw = sl.nd + hw * M;
                             int4 *stk = (int4 *)(sl.lines + hw * M);
                             float *xch = (float *)(sl.proj + hw * M);   // 2 x (A / 2) entries of (x, y, a)
                             const float SX = (float)HF(sl, H_PX, hw), SY = (float)HF(sl, H_PY, hw);
-                            float px[4], py[4];
-                            int pa[4], qq[4];
+                            float px[8], py[8];
+                            int pa[8], qq[8];
 #pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                qq[u] = sub + 8 * u;
+                            for (int u = 0; u < 8; ++u) {
+                                qq[u] = sub + 4 * u;
                                 const bool v = qq[u] < A;
                                 const float2 t = v ? ((const float2 *)xch)[qq[u]] : make_float2(0.0f, 0.0f);
                                 px[u] = t.x; py[u] = t.y;
@@ -2209,13 +2195,13 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                             auto red = [&](int b0, int e1, float &mnx, float &mxx, float &mny, float &mxy) {
                                 float a0 = INFINITY, a1 = -INFINITY, c0 = INFINITY, c1 = -INFINITY;
 #pragma unroll
-                                for (int u = 0; u < 4; ++u) {
+                                for (int u = 0; u < 8; ++u) {
                                     if (qq[u] >= b0 && qq[u] < e1) {
                                         a1 = a1 < px[u] ? px[u] : a1; a0 = px[u] < a0 ? px[u] : a0;
                                         c1 = c1 < py[u] ? py[u] : c1; c0 = py[u] < c0 ? py[u] : c0;
                                     }
                                 }
-                                mnx = oct_min(a0); mxx = oct_max(a1); mny = oct_min(c0); mxy = oct_max(c1);
+                                mnx = quad_min(a0); mxx = quad_max(a1); mny = quad_min(c0); mxy = quad_max(c1);
                             };
                             // z: bit 0 = split on x, bit 1 = all points coincide (zero-extent box)
                             auto entry = [&](int b0, int e1, float mnx, float mxx, float mny, float mxy) {
@@ -2240,14 +2226,14 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
 #endif
                                 const int4 en = stk[--sp];
                                 const int b0 = en.x, e1 = en.y;
-                                bool pr[4];
+                                bool pr[8];
                                 if (e1 - b0 <= 10) {   // leaf (RVO_MAX_LEAF_SIZE): insert in position order
 #pragma unroll
-                                    for (int u = 0; u < 4; ++u)
+                                    for (int u = 0; u < 8; ++u)
                                         pr[u] = qq[u] >= b0 && qq[u] < e1 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
                                     const uint32_t bits = gmask(pr);
 #pragma unroll
-                                    for (int u = 0; u < 4; ++u)
+                                    for (int u = 0; u < 8; ++u)
                                         if (pr[u])
                                             tpos[(pa[u] - 1) * HS + hw] =
                                                 (uint8_t)(tc + __popc(bits & ((1u << qq[u]) - 1u)));
@@ -2260,16 +2246,16 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                                     // one-agent leaf, nothing moves, and the equal-distance children are
                                     // visited right first: positions [e1-10, e1) in order, then e1-11 down to b0
 #pragma unroll
-                                    for (int u = 0; u < 4; ++u)
+                                    for (int u = 0; u < 8; ++u)
                                         pr[u] = qq[u] >= e1 - 10 && qq[u] < e1 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
                                     const uint32_t b1 = gmask(pr);
-                                    bool p2[4];
+                                    bool p2[8];
 #pragma unroll
-                                    for (int u = 0; u < 4; ++u)
+                                    for (int u = 0; u < 8; ++u)
                                         p2[u] = qq[u] >= b0 && qq[u] < e1 - 10 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
                                     const uint32_t b2 = gmask(p2);
 #pragma unroll
-                                    for (int u = 0; u < 4; ++u) {
+                                    for (int u = 0; u < 8; ++u) {
                                         if (pr[u])
                                             tpos[(pa[u] - 1) * HS + hw] = (uint8_t)(tc + __popc(b1 & ((1u << qq[u]) - 1u)));
                                         if (p2[u])
@@ -2280,15 +2266,15 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                                     continue;
                                 }
                                 const float split = __int_as_float(en.w);
-                                bool lt[4], pL[4], pR[4];
+                                bool lt[8], pL[8], pR[8];
 #pragma unroll
-                                for (int u = 0; u < 4; ++u) {
+                                for (int u = 0; u < 8; ++u) {
                                     lt[u] = ((en.z & 1) ? px[u] : py[u]) < split;
                                     pr[u] = qq[u] >= b0 && qq[u] < e1 && lt[u];
                                 }
                                 const int mid = b0 + __popc(gmask(pr));
 #pragma unroll
-                                for (int u = 0; u < 4; ++u) {
+                                for (int u = 0; u < 8; ++u) {
                                     const bool in = qq[u] >= b0 && qq[u] < e1;
                                     pL[u] = in && qq[u] < mid && !lt[u];
                                     pR[u] = in && qq[u] >= mid && lt[u];
@@ -2296,9 +2282,9 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                                 const uint32_t Lm = gmask(pL), Rm = gmask(pR);
                                 if (Lm) {
                                     const int nsw = __popc(Lm);
-                                    int slot[4];
+                                    int slot[8];
 #pragma unroll
-                                    for (int u = 0; u < 4; ++u) {
+                                    for (int u = 0; u < 8; ++u) {
                                         slot[u] = pL[u] ? __popc(Lm & ((1u << qq[u]) - 1u))
                                                         : nsw + __popc(Rm >> qq[u] >> 1);
                                         if (pL[u] || pR[u]) {
@@ -2308,7 +2294,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                                     }
                                     wsync();
 #pragma unroll
-                                    for (int u = 0; u < 4; ++u) {
+                                    for (int u = 0; u < 8; ++u) {
                                         if (pL[u] || pR[u]) {
                                             const float *o = xch + 3 * (pL[u] ? slot[u] + nsw : slot[u] - nsw);
                                             px[u] = o[0]; py[u] = o[1]; pa[u] = __float_as_int(o[2]);
@@ -2331,7 +2317,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                                 wsync();
                             }
 #pragma unroll
-                            for (int u = 0; u < 4; ++u)
+                            for (int u = 0; u < 8; ++u)
                                 if (qq[u] < A) S.o_perm[gw * A + qq[u]] = (uint8_t)pa[u];
 #ifdef CN_STAMPS
                             if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + 13] = dbg_it;
