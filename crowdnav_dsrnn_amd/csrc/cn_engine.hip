@@ -94,7 +94,9 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     // each quad) that fixes RVO2's neighbour order.
     p.T = CN_BLK;
     p.H = 64;
-    p.EPB = p.H / N;
+    // at most 16 envs per workgroup: with 1-3 humans per env (side-preference scenarios) 64 / N envs would
+    // put up to 64 env lanes' divergent reward / norm-zone work on one wave (C5: 16 -> +6 %; 8 -> -2 %)
+    p.EPB = p.H / N < 16 ? p.H / N : 16;
     const int H = p.H;
     const int ML = p.M > 0 ? p.M : 1;
     int o = 0;
