@@ -368,15 +368,39 @@ __device__ __forceinline__ bool disc_quad_sat(double px, double py, double r, co
         for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
         if (amax < bmin || bmax < amin) return false;
     }
-    for (int k = 0; k < 64; ++k) {  // 64-gon edge k -> k+1: its normal (-ey, ex) points at angle -(k + 1/2) pi/32
-        const double ex = gon_x(px, r, k + 1) - gon_x(px, r, k), ey = gon_y(py, r, k + 1) - gon_y(py, r, k);
-        if (ex == 0.0 && ey == 0.0) continue;
-        const double nx = -ey, ny = ex;
-        double amin, amax, bmin = INFINITY, bmax = -INFINITY;
-        gon_extent(px, py, r, nx, ny, k, amin, amax);
+    // 64-gon edge k -> k+1: its normal (-ey, ex) points at angle -(k + 1/2) pi/32. The loop index is
+    // wave-uniform, so the unit-circle entries of the +-2 windows (vertices k-2..k+2 and k+30..k+34, as in
+    // gon_extent) slide along in registers and the two new entries are loaded one iteration ahead: the
+    // loop was bound by the latency of its table loads. Same vertices, same operations.
+    double wc[5], ws[5], oc[5], os[5];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
-        if (amax < bmin || bmax < amin) return false;
+    for (int i = 0; i < 5; ++i) {
+        wc[i] = c_circ_cos[(i - 2) & 63]; ws[i] = c_circ_sin[(i - 2) & 63];
+        oc[i] = c_circ_cos[(30 + i) & 63]; os[i] = c_circ_sin[(30 + i) & 63];
+    }
+    auto vx = [&](int idx, double cs) { return (idx & 63) == 0 ? px + r : px + r * cs; };
+    auto vy = [&](int idx, double sn) { return (idx & 63) == 0 ? py : py + r * sn; };
+    for (int k = 0; k < 64; ++k) {
+        const double nc = c_circ_cos[(k + 3) & 63], ns = c_circ_sin[(k + 3) & 63];
+        const double nco = c_circ_cos[(k + 35) & 63], nso = c_circ_sin[(k + 35) & 63];
+        const double ex = vx(k + 1, wc[3]) - vx(k, wc[2]), ey = vy(k + 1, ws[3]) - vy(k, ws[2]);
+        if (!(ex == 0.0 && ey == 0.0)) {
+            const double nx = -ey, ny = ex;
+            double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+#pragma unroll
+            for (int d = 0; d < 5; ++d) {
+                const double t = vx(k - 2 + d, wc[d]) * nx + vy(k - 2 + d, ws[d]) * ny;
+                const double u = vx(k + 30 + d, oc[d]) * nx + vy(k + 30 + d, os[d]) * ny;
+                amax = t > amax ? t : amax;
+                amin = u < amin ? u : amin;
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
+            if (amax < bmin || bmax < amin) return false;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { wc[i] = wc[i + 1]; ws[i] = ws[i + 1]; oc[i] = oc[i + 1]; os[i] = os[i + 1]; }
+        wc[4] = nc; ws[4] = ns; oc[4] = nco; os[4] = nso;
     }
     return true;
 }
