@@ -157,3 +157,34 @@ def test_gpu_mixed_c5_vs_oracle(gpu_mixed, oracle):
         np.testing.assert_array_equal(g_out[4][:, abi.INFO_PATH_VIOLATION], r_out[4][:, abi.INFO_PATH_VIOLATION])
         np.testing.assert_array_equal(g_out[4][:, abi.INFO_SCENARIO], r_out[4][:, abi.INFO_SCENARIO])
     assert flips <= E * 60 * 0.001, flips
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_stream_ordering():
+    """The mixed engine forks its group launches off the caller's stream and joins them back: work queued on
+    the caller's (non-default) stream right after cn_step sees every group's outputs, with no device-wide
+    synchronisation in between (compared with the same engine stepped and synchronised step by step)."""
+    import torch
+
+    from crowdnav_dsrnn_amd.engine import CrowdNavEngine
+
+    E = 1000
+    cfgs, eg = bench.c5_mixed(E, 0, E)
+    a, b = CrowdNavEngine.mixed(cfgs, eg), CrowdNavEngine.mixed(cfgs, eg)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    acts = torch.randn((30, E, 2), generator=g, device="cuda") * 0.5
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        a.reset()
+        snaps = []
+        for t in range(30):
+            obs, rew, done = a.step(acts[t])[:3]
+            snaps.append((obs["spatial_edges"].clone(), rew.clone(), done.clone()))   # queued on s after the join
+    b.reset()
+    torch.cuda.synchronize()
+    for t in range(30):
+        obs, rew, done = b.step(acts[t])[:3]
+        torch.cuda.synchronize()
+        s.synchronize()
+        assert torch.equal(snaps[t][0], obs["spatial_edges"]) and torch.equal(snaps[t][1], rew), t
+        assert torch.equal(snaps[t][2], done), t
