@@ -206,33 +206,57 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_{32x32x2,16x16
 
 
 def gru_gemm_roofline(torch, device, B, H, reps=50):
-    """Roofline of C4's dominant kernel: the per-step recurrent GEMM of the spatial-edge GRU in the PPO
-    update (ops._MaskedGRU: gh = hm W_hh^T + b_hh, B = envs per minibatch x humans rows, K = H = 256,
-    3H = 768 columns; 128 steps x 5 epochs x 2 minibatches per update, plus the backward's acc += dgh
-    W_hh of the same size). The same call on the same shapes is timed with HIP events on the stream it
-    runs on; algorithmic FLOP per launch = 2 B H 3H."""
+    """Roofline of C4's dominant forward kernel: the per-step fused recurrent step of the spatial-edge GRU
+    in the PPO update (ops._MaskedGRU -> cn_gru_fwd_fused: gh = hm W_hh^T + b_hh on the f32 MFMA with the
+    gate epilogue, B = envs per minibatch x humans rows, K = H = 256, 3H = 768 columns; 128 steps x 5 epochs
+    x 2 minibatches per update). The same call on the same shapes (save record and next masked state
+    written, as in training) is timed with HIP events on the stream it runs on; algorithmic FLOP per launch
+    = 2 B H 3H (the gate arithmetic is not counted). The unfused pair it replaced (hipBLASLt addmm +
+    cn_gru_fwd_step) is timed beside it."""
+    from crowdnav_dsrnn_amd import _lib
+    L = _lib.lib()
     g = torch.Generator(device=device)
     g.manual_seed(1)
     hm = torch.randn((B, H), generator=g, device=device)
     w = torch.randn((3 * H, H), generator=g, device=device) * 0.05
     b = torch.randn((3 * H,), generator=g, device=device)
-    out = torch.empty((B, 3 * H), device=device)
-    for _ in range(5):
-        torch.addmm(b, hm, w.t(), out=out)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        torch.addmm(b, hm, w.t(), out=out)
-    e1.record()
-    e1.synchronize()
-    dt = e0.elapsed_time(e1) / 1e3 / reps
+    gi = torch.randn((B, 3 * H), generator=g, device=device)
+    m = torch.ones((B,), device=device)
+    h_out = torch.empty((B, H), device=device)
+    hm_next = torch.empty((B, H), device=device)
+    save = torch.empty((B, 4 * H), device=device)
+    gh = torch.empty((B, 3 * H), device=device)
+    st = torch.cuda.current_stream(device).cuda_stream
+
+    def fused():
+        _lib.check(L.cn_gru_fwd_fused(st, B, H, gi.data_ptr(), hm.data_ptr(), w.data_ptr(), b.data_ptr(),
+                                      m.data_ptr(), h_out.data_ptr(), hm_next.data_ptr(), save.data_ptr(), None, 1, 0))
+
+    def pair():
+        torch.addmm(b, hm, w.t(), out=gh)
+        _lib.check(L.cn_gru_fwd_step(st, B, H, gi.data_ptr(), gh.data_ptr(), hm.data_ptr(), m.data_ptr(),
+                                     h_out.data_ptr(), hm_next.data_ptr(), save.data_ptr()))
+
+    def timed(fn):
+        for _ in range(5):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) / 1e3 / reps
+
+    dt, dt_pair = timed(fused), timed(pair)
     flop = 2.0 * B * H * 3 * H
     tf = flop / dt / 1e12
     return {"bound": "mfma", "achieved": round(tf, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(tf / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-            "kernel": "spatial-edge GRU step GEMM gh = hm W_hh^T + b_hh (hipBLASLt fp32 MFMA), %d x %d -> %d"
-                      % (B, H, 3 * H),
-            "flop_per_launch": flop, "avg_launch_us": round(dt * 1e6, 2)}
+            "kernel": "spatial-edge GRU fused step cn_gru_fwd_fused (gh = hm W_hh^T + b_hh on the fp32 MFMA + gates), "
+                      "%d x %d -> %d" % (B, H, 3 * H),
+            "flop_per_launch": flop, "avg_launch_us": round(dt * 1e6, 2),
+            "unfused_addmm_plus_gates_us": round(dt_pair * 1e6, 2)}
 
 
 def run_c4(args, torch, dist, device, rank, world):

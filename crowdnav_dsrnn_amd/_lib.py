@@ -72,6 +72,7 @@ def lib():
     L.cn_edge_features.argtypes = [vp, i64, ctypes.c_int] + [vp] * 14
     L.cn_gru_fwd_step.argtypes = [vp, i64, ctypes.c_int] + [vp] * 7
     L.cn_gru_fwd_step_scatter.argtypes = [vp, i64, ctypes.c_int] + [vp] * 8 + [i64, i64]
+    L.cn_gru_fwd_fused.argtypes = [vp, i64, ctypes.c_int] + [vp] * 9 + [i64, i64]
     L.cn_debug_disc_quad.argtypes = [vp, i64, ctypes.c_int] + [vp] * 6
     L.cn_debug_orca.argtypes = [vp, i64, ctypes.c_int, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp]
     L.cn_debug_copy64.argtypes = [vp, i64, ctypes.c_int, vp, vp]
@@ -86,7 +87,7 @@ def lib():
                                   ctypes.POINTER(i64)]
     for f in ("cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
               "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features", "cn_profile",
-              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_social_force_predict"):
+              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_social_force_predict"):
         getattr(L, f).restype = i32
     _lib = L
     return L
@@ -102,5 +103,5 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_destroy", "cn_reset", "cn_step",
             "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
             "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter",
-            "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad",
+            "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad",
             "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_social_force_predict"]

@@ -121,6 +121,185 @@ __global__ __launch_bounds__(256) void cn_gru_bwd_kernel(int64_t B, int H, float
 
 inline unsigned grid_for(int64_t B, int H) { return (unsigned)((B * (H / 4) + 255) / 256); }
 
+// ------------------------------------------------------------------------------------------------
+// Fused recurrent step: gh = hm W_hh^T + b_hh on the f32-input matrix cores with the gate arithmetic of
+// cn_gru_fwd_kernel in the epilogue, so gh ([B][3H], 63 MB at C4's 20,480 x 256) never goes to HBM.
+// Workgroup tile: GF_BM = 128 rows x GF_BU = 32 hidden units, i.e. the r, z and n columns of those units
+// (96 of W_hh's rows); 4 waves, wave w owns rows 32w .. 32w + 31 and one 32x32 accumulator per gate
+// (v_mfma_f32_32x32x2_f32: exact f32 products, f32 accumulation). K (= H) streams through LDS in chunks
+// of 32, double-buffered: the next chunk's global loads are in flight while the current one is multiplied.
+// The k pair of an MFMA is a permutation of K (lane half p of step (c, q) holds k = 8c + 4p + q for A
+// and B alike), so every lane reads 16-byte LDS vectors. Rows are padded to 36 floats in LDS (the 32 rows
+// of a b128 read land on distinct bank groups).
+// Grid: XCD-aware -- workgroup id x runs on XCD x % 8; the 8 unit tiles (H = 256) of one row tile are
+// given consecutive ids on the same XCD, so the row tile's hm rows are fetched into that XCD's L2 once.
+// ------------------------------------------------------------------------------------------------
+constexpr int GF_BM = 128, GF_BU = 32, GF_KC = 32, GF_LD = GF_KC + 4;
+typedef float gf_f32x16 __attribute__((ext_vector_type(16)));
+
+__global__ __launch_bounds__(256, 2) void cn_gru_fused_kernel(int64_t B, int H, int row_tiles, int unit_tiles,
+                                                              const float *__restrict__ gi,
+                                                              const float *__restrict__ hm,
+                                                              const float *__restrict__ w_hh,
+                                                              const float *__restrict__ b_hh,
+                                                              const float *__restrict__ m_next,
+                                                              float *__restrict__ h_out, float *__restrict__ hm_next,
+                                                              float *__restrict__ save, float *__restrict__ h_out2,
+                                                              int64_t g2, int64_t ld2)
+{
+    // LDS: the double-buffered A / B chunks during the K loop, then the three gate accumulators of the tile
+    // (sC[g][row][unit], rows padded to GF_LD) for the epilogue's row-major pass.
+    constexpr int SA = GF_BM * GF_LD, SB = 3 * GF_BU * GF_LD;
+    constexpr int SMEM = 2 * (SA + SB) > 3 * GF_BM * GF_LD ? 2 * (SA + SB) : 3 * GF_BM * GF_LD;
+    __shared__ __attribute__((aligned(16))) float smem[SMEM];
+    float *const sA0 = smem, *const sB0 = smem + 2 * SA;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, k = bid >> 3;
+    const int ut = k % unit_tiles;
+    const int rt = (k / unit_tiles) * 8 + xcd;
+    if (rt >= row_tiles) return;  // grid padding (whole workgroup, before any barrier)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t row0 = (int64_t)rt * GF_BM;
+    const int u0 = ut * GF_BU;
+
+    // global -> register staging: A = 128 rows x 32 floats (4 float4 per thread), B = 96 rows (3 per thread).
+    // Plain scalars (no captured arrays): the loads must stay in flight across the chunk's MFMAs. The same
+    // thread -> (row, 4 columns) map serves the epilogue: thread t owns units u0 + lc .. + 3 of rows lr + 32 i.
+    const int lc = (tid & 7) * 4, lr = tid >> 3;
+    // rows past B (last row tile) read row B - 1 instead: rows are independent and those are never stored
+    int64_t ar[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ar[i] = min(row0 + lr + 32 * i, B - 1);
+    const float *pa0 = hm + ar[0] * H + lc, *pa1 = hm + ar[1] * H + lc, *pa2 = hm + ar[2] * H + lc,
+                *pa3 = hm + ar[3] * H + lc;
+    const float *pb0 = w_hh + (int64_t)(u0 + lr) * H + lc;
+    const int64_t b_step = (int64_t)H * H;
+    float4 ra0, ra1, ra2, ra3, rb0, rb1, rb2;
+#define GF_GLOAD(kc)                                                         \
+    ra0 = *(const float4 *)(pa0 + (kc));                                     \
+    ra1 = *(const float4 *)(pa1 + (kc));                                     \
+    ra2 = *(const float4 *)(pa2 + (kc));                                     \
+    ra3 = *(const float4 *)(pa3 + (kc));                                     \
+    rb0 = *(const float4 *)(pb0 + (kc));                                     \
+    rb1 = *(const float4 *)(pb0 + b_step + (kc));                            \
+    rb2 = *(const float4 *)(pb0 + 2 * b_step + (kc));
+#define GF_LSTORE(buf)                                                                    \
+    {                                                                                     \
+        float *da = sA0 + (buf) * SA + lr * GF_LD + lc, *db = sB0 + (buf) * SB + lr * GF_LD + lc; \
+        *(float4 *)(da) = ra0;                                                            \
+        *(float4 *)(da + 32 * GF_LD) = ra1;                                               \
+        *(float4 *)(da + 64 * GF_LD) = ra2;                                               \
+        *(float4 *)(da + 96 * GF_LD) = ra3;                                               \
+        *(float4 *)(db) = rb0;                                                            \
+        *(float4 *)(db + GF_BU * GF_LD) = rb1;                                            \
+        *(float4 *)(db + 2 * GF_BU * GF_LD) = rb2;                                        \
+    }
+    const int li = lane & 31, p4 = (lane >> 5) * 4;
+#define GF_MMA(buf)                                                                                          \
+    {                                                                                                        \
+        const float *a_base = sA0 + (buf) * SA + (wave * 32 + li) * GF_LD + p4;                              \
+        const float *b_base = sB0 + (buf) * SB + li * GF_LD + p4;                                            \
+        _Pragma("unroll") for (int c = 0; c < GF_KC / 8; ++c)                                                \
+        {                                                                                                    \
+            const float4 a = *(const float4 *)(a_base + 8 * c);                                              \
+            float4 bv[3];                                                                                    \
+            _Pragma("unroll") for (int g = 0; g < 3; ++g) bv[g] = *(const float4 *)(b_base + g * GF_BU * GF_LD + 8 * c); \
+            _Pragma("unroll") for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bv[g].x, acc[g], 0, 0, 0); \
+            _Pragma("unroll") for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bv[g].y, acc[g], 0, 0, 0); \
+            _Pragma("unroll") for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bv[g].z, acc[g], 0, 0, 0); \
+            _Pragma("unroll") for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bv[g].w, acc[g], 0, 0, 0); \
+        }                                                                                                    \
+    }
+
+    gf_f32x16 acc[3];
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[g][e] = 0.0f;
+
+    const int nch = H / GF_KC;
+    GF_GLOAD(0)
+    GF_LSTORE(0)
+    __syncthreads();
+    for (int ch = 0; ch + 1 < nch; ++ch) {
+        GF_GLOAD((ch + 1) * GF_KC)
+        GF_MMA(ch & 1)
+        GF_LSTORE((ch + 1) & 1)
+        __syncthreads();
+    }
+    // last chunk: the epilogue's operands (gi's three gate blocks and hm of this thread's 4 x 4 outputs) are
+    // fetched while its MFMAs run
+    float4 eg[4][3], eh[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float *gib = gi + ar[i] * 3 * H + u0 + lc;
+#pragma unroll
+        for (int g = 0; g < 3; ++g) eg[i][g] = *(const float4 *)(gib + g * H);
+        eh[i] = *(const float4 *)(hm + ar[i] * H + u0 + lc);
+    }
+    GF_MMA((nch - 1) & 1)
+    __syncthreads();  // every wave is done reading the chunk buffers before sC overwrites them
+#undef GF_GLOAD
+#undef GF_LSTORE
+#undef GF_MMA
+
+    // accumulators -> LDS: lane holds unit li of rows (e & 3) + 8 (e >> 2) + 4 (lane >> 5) of its wave's 32
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+            smem[(g * GF_BM + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * GF_LD + li] = acc[g][e];
+    __syncthreads();
+
+    const float4 br = *(const float4 *)(b_hh + u0 + lc), bz = *(const float4 *)(b_hh + H + u0 + lc),
+                 bn = *(const float4 *)(b_hh + 2 * H + u0 + lc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = lr + 32 * i;
+        const int64_t b = row0 + row;
+        if (b >= B) continue;
+        const float4 cr = *(const float4 *)(smem + (0 * GF_BM + row) * GF_LD + lc);
+        const float4 cz = *(const float4 *)(smem + (1 * GF_BM + row) * GF_LD + lc);
+        const float4 cn = *(const float4 *)(smem + (2 * GF_BM + row) * GF_LD + lc);
+#ifdef CN_GF_PROBE_NOEPI  // diagnostic build (tools/gru_fused_probe.hip): the GEMM loop + LDS pass alone
+        *(float4 *)(h_out + b * H + u0 + lc) = make_float4(cr.x + cz.x + cn.x, cr.y, cz.z, cn.w);
+        continue;
+#endif
+        const float4 ir = eg[i][0], iz = eg[i][1], in = eg[i][2], hp = eh[i];
+        float4 hr, hz, hn, r, z, n, h;
+#define CN_GATE(c)                                 \
+    hr.c = cr.c + br.c;                            \
+    hz.c = cz.c + bz.c;                            \
+    hn.c = cn.c + bn.c;                            \
+    r.c = sigm(hr.c + ir.c);                       \
+    z.c = sigm(hz.c + iz.c);                       \
+    n.c = tanhf(in.c + hn.c * r.c);                \
+    h.c = (hp.c - n.c) * z.c + n.c;
+        CN_GATE(x) CN_GATE(y) CN_GATE(z) CN_GATE(w)
+#undef CN_GATE
+        const int64_t o = b * H + u0 + lc;
+        *(float4 *)(h_out + o) = h;
+        if (h_out2) {
+            float *d = h_out2 + (b / g2) * ld2 + (b % g2) * H + u0 + lc;
+            d[0] = h.x;
+            d[1] = h.y;
+            d[2] = h.z;
+            d[3] = h.w;
+        }
+        if (hm_next) {
+            const float m = m_next ? m_next[b] : 1.0f;
+            *(float4 *)(hm_next + o) = make_float4(h.x * m, h.y * m, h.z * m, h.w * m);
+        }
+        if (save) {
+            float *sv = save + b * 4 * H + u0 + lc;
+            *(float4 *)(sv) = r;
+            *(float4 *)(sv + H) = z;
+            *(float4 *)(sv + 2 * H) = n;
+            *(float4 *)(sv + 3 * H) = hn;
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -142,6 +321,26 @@ int cn_gru_fwd_step_scatter(void *stream, int64_t B, int H, const float *gi, con
         return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_scatter: g2 > 0, ld2 >= g2 * H, ld2 % 4 == 0, 16-byte aligned h_out2");
     hipLaunchKernelGGL(cn_gru_fwd_kernel, dim3(grid_for(B, H)), dim3(256), 0, (hipStream_t)stream, B, H, gi, gh,
                        hm, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+int cn_gru_fwd_fused(void *stream, int64_t B, int H, const float *gi, const float *hm, const float *w_hh,
+                     const float *b_hh, const float *m_next, float *h_out, float *hm_next, float *save, float *h_out2,
+                     int64_t g2, int64_t ld2)
+{
+    if (B <= 0 || H <= 0 || H % GF_BU) return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: B > 0 and H % 32 == 0 required");
+    if (!gi || !hm || !w_hh || !b_hh || !h_out) return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: null operand");
+    if ((((uintptr_t)hm) | ((uintptr_t)w_hh)) & 15)
+        return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: hm and w_hh must be 16-byte aligned");
+    if (h_out2 && (g2 <= 0 || ld2 < g2 * H))
+        return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: g2 > 0 and ld2 >= g2 * H required");
+    const int64_t rt = (B + GF_BM - 1) / GF_BM;
+    const int ut = H / GF_BU;
+    const int64_t grid = (rt + 7) / 8 * 8 * ut;
+    if (grid > 0x7fffffff) return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: B too large");
+    hipLaunchKernelGGL(cn_gru_fused_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, B, H, (int)rt, ut,
+                       gi, hm, w_hh, b_hh, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }

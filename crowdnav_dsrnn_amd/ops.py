@@ -7,9 +7,10 @@ linear(...)         — nn.Linear with a split-K weight gradient (library GEMMs;
                       T*B or T*B*N rows in training, where dW = dY^T X has a tiny output and K ~ 10^6).
 attention_pool(...) — EdgeAttention's weighted sum of the spatial edge states (cn_attn_pool_*).
 masked_gru(...)     — the mask-segmented GRU of the three DSRNN RNNs over a (T, B) sequence
-                      (cn_gru_fwd_step / cn_gru_bwd_step + library GEMMs), with its own backward.
+                      (cn_gru_fwd_fused: recurrent GEMM on the f32 matrix cores + gates in one launch per
+                      step; cn_gru_bwd_step + library GEMMs backward), with its own backward.
 gru_infer_step(...) — one no-autograd step of the same GRU for act(): reads the state through strided views
-                      and writes the new state straight into the (B, N + 1, H) layout (cn_gru_fwd_step_scatter).
+                      and writes the new state straight into the (B, N + 1, H) layout (cn_gru_fwd_fused).
 """
 import torch
 
@@ -121,9 +122,10 @@ def linear(x, W, b=None):
 class _MaskedGRU(torch.autograd.Function):
     """srnn_model.py:52-104 (RNNBase._forward_gru): h <- h * mask[t] before step t, then one nn.GRU step.
 
-    Forward: gi = x W_ih^T + b_ih as one GEMM over all T*B rows; per step one GEMM gh = hm W_hh^T + b_hh
-    and one cn_gru_fwd_step (gates, new state, next masked state; saves r|z|n|gh_n when a gradient is
-    needed). Backward: per step (reversed) one cn_gru_bwd_step and one GEMM acc += dgh W_hh, then the
+    Forward: gi = x W_ih^T + b_ih as one GEMM over all T*B rows; per step one cn_gru_fwd_fused (the
+    recurrent GEMM gh = hm W_hh^T + b_hh on the f32 matrix cores with the gates, new state, next masked
+    state and the r|z|n|gh_n record for backward in its epilogue; H % 32 != 0: a library GEMM + the
+    cn_gru_fwd_step gate kernel). Backward: per step (reversed) one cn_gru_bwd_step and one GEMM acc += dgh W_hh, then the
     weight / input gradients as single GEMMs over all T*B rows."""
 
     @staticmethod
@@ -145,17 +147,24 @@ class _MaskedGRU(torch.autograd.Function):
             hm = torch.empty((min(T, 2), B, H), dtype=torch.float32, device=dev)
             save = None
         torch.mul(h0, m[0].unsqueeze(-1), out=hm[0])
-        gh = torch.empty((B, 3 * H), dtype=torch.float32, device=dev)
+        fused = H % 32 == 0
+        gh = None if fused else torch.empty((B, 3 * H), dtype=torch.float32, device=dev)
+        whh, bhh = _c(w_hh), _c(b_hh)
         nh = hm.shape[0]
         with torch.cuda.device(dev):
             for t in range(T):
                 cur = hm[t % nh]
-                torch.addmm(b_hh, cur, w_hh.t(), out=gh)
                 last = t + 1 == T
-                _lib.check(L.cn_gru_fwd_step(st, B, H, gi[t].data_ptr(), gh.data_ptr(), cur.data_ptr(),
-                                             None if last else m[t + 1].data_ptr(), out[t].data_ptr(),
-                                             None if last else hm[(t + 1) % nh].data_ptr(),
-                                             save[t].data_ptr() if need else None))
+                mn = None if last else m[t + 1].data_ptr()
+                hn = None if last else hm[(t + 1) % nh].data_ptr()
+                sv = save[t].data_ptr() if need else None
+                if fused:
+                    _lib.check(L.cn_gru_fwd_fused(st, B, H, gi[t].data_ptr(), cur.data_ptr(), whh.data_ptr(),
+                                                  bhh.data_ptr(), mn, out[t].data_ptr(), hn, sv, None, 1, 0))
+                else:
+                    torch.addmm(b_hh, cur, w_hh.t(), out=gh)
+                    _lib.check(L.cn_gru_fwd_step(st, B, H, gi[t].data_ptr(), gh.data_ptr(), cur.data_ptr(), mn,
+                                                 out[t].data_ptr(), hn, sv))
         if need:
             ctx.save_for_backward(x2, m, w_ih, w_hh, hm, save)
         return out, out[-1].clone()
@@ -212,7 +221,8 @@ def gru_infer_step(x, h0, m, w_ih, w_hh, b_ih, b_hh, dest):
     hm = torch.empty((Rg, G, H), dtype=torch.float32, device=dev)
     torch.mul(h0g, m.reshape(Rg, 1, 1), out=hm)
     gi = torch.addmm(b_ih, _c(x).reshape(R, -1), w_ih.t())
-    gh = torch.addmm(b_hh, hm.view(R, H), w_hh.t())
+    fused = H % 32 == 0
+    gh = None if fused else torch.addmm(b_hh, hm.view(R, H), w_hh.t())
     out = torch.empty((R, H), dtype=torch.float32, device=dev)
     d_ptr, ld = None, 0
     if dest is not None:
@@ -221,8 +231,14 @@ def gru_infer_step(x, h0, m, w_ih, w_hh, b_ih, b_hh, dest):
             raise ValueError("gru_infer_step: dest must be a float32 (R', G, H) view with rows of H contiguous")
         d_ptr, ld = dg.data_ptr(), dg.stride(0)
     with torch.cuda.device(dev):
-        _lib.check(_lib.lib().cn_gru_fwd_step_scatter(_stream(dev), R, H, gi.data_ptr(), gh.data_ptr(), hm.data_ptr(),
-                                                   None, out.data_ptr(), None, None, d_ptr, G, ld))
+        if fused:
+            _lib.check(_lib.lib().cn_gru_fwd_fused(_stream(dev), R, H, gi.data_ptr(), hm.data_ptr(), _c(w_hh).data_ptr(),
+                                                   _c(b_hh).data_ptr(), None, out.data_ptr(), None, None, d_ptr, G,
+                                                   ld))
+        else:
+            _lib.check(_lib.lib().cn_gru_fwd_step_scatter(_stream(dev), R, H, gi.data_ptr(), gh.data_ptr(),
+                                                          hm.data_ptr(), None, out.data_ptr(), None, None, d_ptr, G,
+                                                          ld))
     return out
 
 

@@ -225,6 +225,15 @@ int cn_gru_fwd_step_scatter(void *stream, int64_t B, int H, const float *gi, con
                          const float *m_next, float *h_out, float *hm_next, float *save, float *h_out2, int64_t g2,
                          int64_t ld2);
 
+/* Fused step: the recurrent GEMM gh = hm W_hh^T + b_hh (w_hh [3H][H] row-major, as nn.GRU's weight_hh_l0;
+ * b_hh [3H]) on the f32 matrix cores with cn_gru_fwd_step_scatter's gate epilogue, so gh never leaves the
+ * chip. Same outputs and arguments as cn_gru_fwd_step_scatter otherwise; H % 32 == 0, hm and w_hh
+ * 16-byte aligned with rows of H contiguous. Replaces torch.addmm + cn_gru_fwd_step per time step of
+ * srnn_model.py:52-104's nn.GRU. */
+int cn_gru_fwd_fused(void *stream, int64_t B, int H, const float *gi, const float *hm, const float *w_hh,
+                     const float *b_hh, const float *m_next, float *h_out, float *hm_next, float *save, float *h_out2,
+                     int64_t g2, int64_t ld2);
+
 /* Gradient of one step. In: acc [B][H] = dL/dhm of the later step (or dL/dh_T at the last step, with
  * m_next = NULL), m_next [B] that later step's mask, dout [B][H] = dL/dh_t from the outputs (NULL = 0),
  * save / hm as written by the forward. Out: dgi, dgh [B][3H] (pre-activation gradients of gi, gh) and

@@ -158,7 +158,8 @@ def test_edge_features_backward_vs_fp32():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T,B,F,H", [(1, 45, 64, 256), (9, 33, 64, 256), (16, 70, 128, 128)])
+@pytest.mark.parametrize("T,B,F,H", [(1, 45, 64, 256), (9, 33, 64, 256), (16, 70, 128, 128), (3, 1000, 32, 64),
+                                     (4, 50, 16, 36)])
 def test_masked_gru_kernels_vs_fp64(T, B, F, H):
     """cn_gru_fwd_step / cn_gru_bwd_step (+ GEMMs) vs the plain torch restatement of the mask-segmented GRU
     (srnn_model.py:52-104) in float64: outputs, final state and every input / weight gradient, with episode
@@ -213,3 +214,44 @@ def test_attention_pool_kernels_vs_fp64(R, N, H):
     want = run(attention_pool_ref, "cpu", torch.float64)
     for n, a, b in zip(("out", "d_hs", "d_attn"), got, want):
         np.testing.assert_allclose(a.numpy(), b.numpy(), atol=1e-5 * max(1.0, float(b.abs().max())), rtol=0, err_msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,G", [(20480, 256, 10), (4099, 128, 1), (1, 256, 1), (130, 64, 5)])
+def test_gru_fused_step_vs_gemm_plus_gates(B, H, G):
+    """cn_gru_fwd_fused (recurrent GEMM on the f32 MFMA + gate epilogue) vs torch.addmm + cn_gru_fwd_step_scatter
+    on the same operands, every output: h_out, the grouped second copy h_out2, hm_next = h * m_next and the
+    r | z | n | gh_n record. Only the GEMM's summation order differs (both f32 products / accumulation):
+    atol 2e-6 on the gates and states of unit-scale operands. B = 20,480 x 256 is C4's spatial-edge step;
+    4099 / 1 / 130 are ragged row tiles (128 rows per workgroup)."""
+    from crowdnav_dsrnn_amd import _lib
+
+    dev = "cuda:0"
+    g = torch.Generator(device=dev)
+    g.manual_seed(B + H)
+    gi = torch.randn((B, 3 * H), generator=g, device=dev)
+    hm = torch.randn((B, H), generator=g, device=dev) * 0.5
+    w = torch.randn((3 * H, H), generator=g, device=dev) / H ** 0.5
+    b = torch.randn((3 * H,), generator=g, device=dev) * 0.1
+    m = (torch.rand((B,), generator=g, device=dev) > 0.3).float()
+    Rg = (B + G - 1) // G
+    L = _lib.lib()
+    st = torch.cuda.current_stream().cuda_stream
+
+    def outs():
+        return [torch.full((B, H), float("nan"), device=dev), torch.full((B, H), float("nan"), device=dev),
+                torch.full((B, 4 * H), float("nan"), device=dev), torch.zeros((Rg, G + 1, H), device=dev)]
+
+    ref = outs()
+    gh = torch.addmm(b, hm, w.t())
+    _lib.check(L.cn_gru_fwd_step_scatter(st, B, H, gi.data_ptr(), gh.data_ptr(), hm.data_ptr(), m.data_ptr(),
+                                         ref[0].data_ptr(), ref[1].data_ptr(), ref[2].data_ptr(), ref[3].data_ptr(),
+                                         G, (G + 1) * H))
+    got = outs()
+    _lib.check(L.cn_gru_fwd_fused(st, B, H, gi.data_ptr(), hm.data_ptr(), w.data_ptr(), b.data_ptr(), m.data_ptr(),
+                                  got[0].data_ptr(), got[1].data_ptr(), got[2].data_ptr(), got[3].data_ptr(), G,
+                                  (G + 1) * H))
+    torch.cuda.synchronize()
+    for n, a, r in zip(("h_out", "hm_next", "save", "h_out2"), got, ref):
+        assert torch.isfinite(a).all(), n
+        np.testing.assert_allclose(a.cpu().numpy(), r.cpu().numpy(), atol=2e-6, rtol=0, err_msg=n)
