@@ -127,7 +127,7 @@ inline unsigned grid_for(int64_t B, int H) { return (unsigned)((B * (H / 4) + 25
 // Workgroup tile: GF_BM = 128 rows x GF_BU = 32 hidden units, i.e. the r, z and n columns of those units
 // (96 of W_hh's rows); 4 waves, wave w owns rows 32w .. 32w + 31 and one 32x32 accumulator per gate
 // (v_mfma_f32_32x32x2_f32: exact f32 products, f32 accumulation). K (= H) streams through LDS in chunks
-// of 32, double-buffered: the next chunk's global loads are in flight while the current one is multiplied.
+// of 32: the next chunk's global loads are in flight while the current one is multiplied.
 // The k pair of an MFMA is a permutation of K (lane half p of step (c, q) holds k = 8c + 4p + q for A
 // and B alike), so every lane reads 16-byte LDS vectors. Rows are padded to 36 floats in LDS (the 32 rows
 // of a b128 read land on distinct bank groups).
@@ -137,7 +137,7 @@ inline unsigned grid_for(int64_t B, int H) { return (unsigned)((B * (H / 4) + 25
 constexpr int GF_BM = 128, GF_BU = 32, GF_KC = 32, GF_LD = GF_KC + 4;
 typedef float gf_f32x16 __attribute__((ext_vector_type(16)));
 
-__global__ __launch_bounds__(256, 2) void cn_gru_fused_kernel(int64_t B, int H, int row_tiles, int unit_tiles,
+__global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(int64_t B, int H, int row_tiles, int unit_tiles,
                                                               const float *__restrict__ gi,
                                                               const float *__restrict__ hm,
                                                               const float *__restrict__ w_hh,
@@ -147,12 +147,14 @@ __global__ __launch_bounds__(256, 2) void cn_gru_fused_kernel(int64_t B, int H, 
                                                               float *__restrict__ save, float *__restrict__ h_out2,
                                                               int64_t g2, int64_t ld2)
 {
-    // LDS: the double-buffered A / B chunks during the K loop, then the three gate accumulators of the tile
-    // (sC[g][row][unit], rows padded to GF_LD) for the epilogue's row-major pass.
-    constexpr int SA = GF_BM * GF_LD, SB = 3 * GF_BU * GF_LD;
-    constexpr int SMEM = 2 * (SA + SB) > 3 * GF_BM * GF_LD ? 2 * (SA + SB) : 3 * GF_BM * GF_LD;
+    // LDS: one A / B chunk buffer during the K loop, then the three gate accumulators of the tile
+    // (sC[g][row][unit], rows padded to LDC = 33) for the epilogue's row-major pass. 50.7 KB in all, so three
+    // workgroups fit per CU: another workgroup's MFMAs cover one's barriers and epilogue (measured 92 us vs
+    // 99 us for the double-buffered 64.5 KB form at two per CU).
+    constexpr int SA = GF_BM * GF_LD, SB = 3 * GF_BU * GF_LD, LDC = 33;
+    constexpr int SMEM = (SA + SB) > 3 * GF_BM * LDC ? (SA + SB) : 3 * GF_BM * LDC;
     __shared__ __attribute__((aligned(16))) float smem[SMEM];
-    float *const sA0 = smem, *const sB0 = smem + 2 * SA;
+    float *const sA0 = smem, *const sB0 = smem + SA;
     const int bid = blockIdx.x;
     const int xcd = bid & 7, k = bid >> 3;
     const int ut = k % unit_tiles;
@@ -222,9 +224,10 @@ __global__ __launch_bounds__(256, 2) void cn_gru_fused_kernel(int64_t B, int H, 
     GF_LSTORE(0)
     __syncthreads();
     for (int ch = 0; ch + 1 < nch; ++ch) {
-        GF_GLOAD((ch + 1) * GF_KC)
-        GF_MMA(ch & 1)
-        GF_LSTORE((ch + 1) & 1)
+        GF_GLOAD((ch + 1) * GF_KC)  // in flight during this chunk's MFMAs
+        GF_MMA(0)
+        __syncthreads();
+        GF_LSTORE(0)
         __syncthreads();
     }
     // last chunk: the epilogue's operands (gi's three gate blocks and hm of this thread's 4 x 4 outputs) are
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(256, 2) void cn_gru_fused_kernel(int64_t B, int H, 
         for (int g = 0; g < 3; ++g) eg[i][g] = *(const float4 *)(gib + g * H);
         eh[i] = *(const float4 *)(hm + ar[i] * H + u0 + lc);
     }
-    GF_MMA((nch - 1) & 1)
+    GF_MMA(0)
     __syncthreads();  // every wave is done reading the chunk buffers before sC overwrites them
 #undef GF_GLOAD
 #undef GF_LSTORE
@@ -248,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void cn_gru_fused_kernel(int64_t B, int H, 
     for (int g = 0; g < 3; ++g)
 #pragma unroll
         for (int e = 0; e < 16; ++e)
-            smem[(g * GF_BM + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * GF_LD + li] = acc[g][e];
+            smem[(g * GF_BM + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * LDC + li] = acc[g][e];
     __syncthreads();
 
     const float4 br = *(const float4 *)(b_hh + u0 + lc), bz = *(const float4 *)(b_hh + H + u0 + lc),
@@ -258,9 +261,12 @@ __global__ __launch_bounds__(256, 2) void cn_gru_fused_kernel(int64_t B, int H, 
         const int row = lr + 32 * i;
         const int64_t b = row0 + row;
         if (b >= B) continue;
-        const float4 cr = *(const float4 *)(smem + (0 * GF_BM + row) * GF_LD + lc);
-        const float4 cz = *(const float4 *)(smem + (1 * GF_BM + row) * GF_LD + lc);
-        const float4 cn = *(const float4 *)(smem + (2 * GF_BM + row) * GF_LD + lc);
+        const float *pcr = smem + (0 * GF_BM + row) * LDC + lc;
+        const float4 cr = make_float4(pcr[0], pcr[1], pcr[2], pcr[3]);
+        const float *pcz = smem + (1 * GF_BM + row) * LDC + lc;
+        const float4 cz = make_float4(pcz[0], pcz[1], pcz[2], pcz[3]);
+        const float *pcn = smem + (2 * GF_BM + row) * LDC + lc;
+        const float4 cn = make_float4(pcn[0], pcn[1], pcn[2], pcn[3]);
 #ifdef CN_GF_PROBE_NOEPI  // diagnostic build (tools/gru_fused_probe.hip): the GEMM loop + LDS pass alone
         *(float4 *)(h_out + b * H + u0 + lc) = make_float4(cr.x + cz.x + cn.x, cr.y, cz.z, cn.w);
         continue;
