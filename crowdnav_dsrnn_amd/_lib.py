@@ -47,6 +47,11 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise NativeLibraryMissing(
             "HIP engine library not built: %s is missing (run `python -m crowdnav_dsrnn_amd.build`)" % LIB_PATH)
+    # torch's HIP runtime first: the library's libamdhip64 dependency then binds to the runtime torch already
+    # loaded (torch ships its own copy). Loaded the other way round, the process holds two HIP runtimes, the
+    # streams and device pointers the host side passes in belong to the other one, and the library's first
+    # launch fails with hipErrorNoDevice.
+    import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     cfgp = ctypes.POINTER(abi.CnConfig)
@@ -77,6 +82,10 @@ def lib():
     L.cn_debug_orca.argtypes = [vp, i64, ctypes.c_int, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp]
     L.cn_debug_copy64.argtypes = [vp, i64, ctypes.c_int, vp, vp]
     L.cn_orca_predict.argtypes = [vp, i64, ctypes.c_int, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp]
+    L.cn_orca_predict_kd.argtypes = [vp, i64, ctypes.c_int, vp, vp, ctypes.c_float, ctypes.c_float, ctypes.c_float, vp,
+                                     vp]
+    L.cn_debug_set_spawn_budget.argtypes = [vp, ctypes.c_longlong]
+    L.cn_debug_spawn_stats.argtypes = [vp, vp]
     L.cn_social_force_predict.argtypes = [vp, i64, ctypes.c_int, vp, vp] + [ctypes.c_double] * 4 + [vp]
     L.cn_gru_bwd_step.argtypes = [vp, i64, ctypes.c_int] + [vp] * 7
     L.cn_lidar_obs.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, vp, vp]
@@ -87,7 +96,7 @@ def lib():
                                   ctypes.POINTER(i64)]
     for f in ("cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
               "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features", "cn_profile",
-              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_social_force_predict"):
+              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict", "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"):
         getattr(L, f).restype = i32
     _lib = L
     return L
@@ -104,4 +113,5 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
             "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter",
             "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_lidar_obs", "cn_debug_disc_quad",
-            "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_social_force_predict"]
+            "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict",
+            "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"]

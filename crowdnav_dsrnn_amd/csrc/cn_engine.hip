@@ -522,8 +522,17 @@ __device__ __forceinline__ int quad_or(int x)
     return x | quad_xor2i(x);
 }
 
-// linearProgram1 on line `no` of Lb (valid lines: bits of vmask), quad-cooperative
-__device__ __forceinline__ bool lp1_q(const float4 *Lb, uint32_t vmask, int no, float radius, int s, float &tL,
+// 64-bit quad OR (MT = uint64_t masks: simulators of more than 32 agents, cn_orca_predict_kd only)
+__device__ __forceinline__ uint32_t quad_or_m(uint32_t x) { return (uint32_t)quad_or((int)x); }
+__device__ __forceinline__ uint64_t quad_or_m(uint64_t x)
+{
+    return (uint64_t)(uint32_t)quad_or((int)(uint32_t)x) | ((uint64_t)(uint32_t)quad_or((int)(uint32_t)(x >> 32)) << 32);
+}
+
+// linearProgram1 on line `no` of Lb (valid lines: bits of vmask), quad-cooperative. MT: the line mask type
+// (uint32_t: <= 32 lines, the step kernel; uint64_t: <= 64, the plugin's large simulators)
+template <typename MT = uint32_t>
+__device__ __forceinline__ bool lp1_q(const float4 *Lb, MT vmask, int no, float radius, int s, float &tL,
                                       float &tR)
 {
     const float4 ln = Lb[no];
@@ -533,7 +542,7 @@ __device__ __forceinline__ bool lp1_q(const float4 *Lb, uint32_t vmask, int no, 
     float ptl = -INFINITY, ptr = INFINITY;
     int pf = 0;
     for (int j = s; j < no; j += 4) {
-        if (!((vmask >> j) & 1u)) continue;
+        if (!((vmask >> j) & (MT)1)) continue;
         const float4 li = Lb[j];
         const float den = det2(ln.z, ln.w, li.z, li.w);
         const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
@@ -554,6 +563,7 @@ __device__ __forceinline__ bool lp1_q(const float4 *Lb, uint32_t vmask, int no, 
 }
 
 // linearProgram2 (optimize closest to (ox, oy)); returns the index of the failing line or n
+template <typename MT = uint32_t>
 __device__ __forceinline__ int lp2_q(const float4 *Lb, int n, float radius, float ox, float oy, int s, float &rx,
                                      float &ry)
 {
@@ -565,7 +575,7 @@ __device__ __forceinline__ int lp2_q(const float4 *Lb, int n, float radius, floa
         const float4 li = Lb[i];
         if (det2(li.z, li.w, li.x - rx, li.y - ry) > 0.0f) {
             float tL, tR;
-            if (!lp1_q(Lb, 0xffffffffu, i, radius, s, tL, tR)) return i;
+            if (!lp1_q<MT>(Lb, ~(MT)0, i, radius, s, tL, tR)) return i;
             const float t = li.z * (ox - li.x) + li.w * (oy - li.y);
             if (t < tL) { rx = li.x + tL * li.z; ry = li.y + tL * li.w; }
             else if (t > tR) { rx = li.x + tR * li.z; ry = li.y + tR * li.w; }
@@ -576,6 +586,7 @@ __device__ __forceinline__ int lp2_q(const float4 *Lb, int n, float radius, floa
 }
 
 // linearProgram3 from line `begin` (agents only); Pb = the human's projected-line scratch
+template <typename MT = uint32_t>
 __device__ __forceinline__ void lp3_q(const float4 *Lb, float4 *Pb, int n, int begin, float radius, int s, float &rx,
                                       float &ry)
 {
@@ -583,25 +594,25 @@ __device__ __forceinline__ void lp3_q(const float4 *Lb, float4 *Pb, int n, int b
     for (int i = begin; i < n; ++i) {
         const float4 li = Lb[i];
         if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
-            int pv = 0;
+            MT pv = 0;
             for (int j = s; j < i; j += 4) {
                 bool v;
                 const float4 pj = proj_line(li, Lb[j], v);
                 Pb[j] = pj;
-                if (v) pv |= 1 << j;
+                if (v) pv |= (MT)1 << j;
             }
-            pv = quad_or(pv);
+            pv = quad_or_m(pv);
             wsync();
             const float tx = rx, ty = ry;
             const float ox = -li.w, oy = li.z;   // linearProgram2(projLines, radius, (-d.y, d.x), true)
             rx = ox * radius; ry = oy * radius;
             bool fail = false;
             for (int k = 0; k < i && !fail; ++k) {
-                if (!((pv >> k) & 1)) continue;
+                if (!((pv >> k) & (MT)1)) continue;
                 const float4 pk = Pb[k];
                 if (det2(pk.z, pk.w, pk.x - rx, pk.y - ry) > 0.0f) {
                     float tL, tR;
-                    if (!lp1_q(Pb, (uint32_t)pv, k, radius, s, tL, tR)) fail = true;
+                    if (!lp1_q<MT>(Pb, pv, k, radius, s, tL, tR)) fail = true;
                     else if (ox * pk.z + oy * pk.w > 0.0f) { rx = pk.x + tR * pk.z; ry = pk.y + tR * pk.w; }
                     else { rx = pk.x + tL * pk.z; ry = pk.y + tL * pk.w; }
                 }
@@ -1330,6 +1341,10 @@ __device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64
 // Store a drawn spawn as env e's pending episode for the reset with key (cc, rc), slot rc & 1.
 // okv: the completing launch's id, or 0 with `prog` = humans placed for a spawn parked mid-way (the
 // stream at the park point, the robot and the first prog humans are stored; resumed by a later launch).
+// FENCE: the kd-tree path, whose spawn waves resume parked spawns and may rewrite a slot that a reset of the
+// same launch reads (the quad path only ever writes the slot of the reset after next: no fences there, each
+// is a write-back of the XCD's L2)
+template <bool FENCE>
 __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_config &c, int64_t E, int64_t e, const Env1 &en, double rth,
                               int sc, uint32_t ovf, const uint32_t *mt_src, int pos, int64_t cc, int32_t rc, int lane,
                               uint32_t okv, int prog)
@@ -1337,6 +1352,13 @@ __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_confi
     const int N = c.human_num;
     const PendPtrs P = pend_slot(P2, rc & 1, E, E * N);
     const int nk = c.rng_mode == CN_RNG_PHILOX ? 1 : CN_MT_N;   // key words to copy
+    // Invalidate the slot before rewriting it, visible device-wide before any new payload or key store:
+    // a reset of the same launch that reads the slot (reset_env: key, fence, then ok) and sees a new key
+    // then sees ok == 0 (or this launch's id) and draws inline instead of reading a half-written payload.
+    if (FENCE) {
+        if (lane == 0) P.ok[e] = 0u;
+        __threadfence();
+    }
     {
         uint32_t v[(CN_MT_N + 63) / 64];
 #pragma unroll
@@ -1354,8 +1376,9 @@ __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_confi
         P.r[e] = en.rpx; P.r[E + e] = en.rpy; P.r[2 * E + e] = en.rgx; P.r[3 * E + e] = en.rgy; P.r[4 * E + e] = rth;
         P.pos[e] = pos; P.ovf[e] = ovf; P.sc[e] = sc; P.cc[e] = cc; P.rc[e] = rc;
         P.prog[e] = okv ? 0 : prog;
-        P.ok[e] = okv;
     }
+    if (FENCE) __threadfence();   // the whole entry before its ok word (release)
+    if (lane == 0) P.ok[e] = okv;
 }
 
 // The deterministic rest of CrowdSimDict.reset (crowd_sim_dict.py:136-203): state of the new episode,
@@ -1638,9 +1661,14 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2,
     const int32_t rc = S.reset_count[e];
     const PendPtrs P = pend_slot(P2, rc & 1, E, E * N);
     // an entry completed by THIS launch (a resumed spawn finishing beside this reset) is not consumed: its
-    // stores need not be visible yet; the reset draws inline instead
+    // stores need not be visible yet; the reset draws inline instead. The key is read BEFORE ok, with an
+    // acquire fence between (GRID: the kd-tree path, the only one whose spawn waves resume parked spawns and
+    // may rewrite this slot during this launch; write_pending zeroes ok and fences before its key stores):
+    // a key written by this launch implies ok == 0 or this launch's id here.
+    const bool key_ok = P.cc[e] == cc && P.rc[e] == rc;
+    if (GRID) __threadfence();
     const uint32_t ok = P.ok[e];
-    if (may_consume && ok && ok != launch_id && P.cc[e] == cc && P.rc[e] == rc) {
+    if (may_consume && ok && ok != launch_id && key_ok) {
         if (lane < N) {
             const int64_t h = e * N + lane, EN = E * N;
             double v[7];
@@ -1685,6 +1713,7 @@ struct PendLaunch {
     OutView ov;             // global env index = c.env_offset + orow(ov, e)
     long long budget;       // clock cycles a spawning wave works before parking (0: never parks)
     uint32_t launch_id;     // nonzero id of this launch (pending entries it completes carry it)
+    uint32_t *stats;        // [4] cumulative (kd-tree path): parked unstarted, parked mid-way, resumed, completed on resume
 };
 
 // GRID: the spawn's crowded rejection through a DiscGrid (the kd-tree path's plans have LDS for it).
@@ -1710,6 +1739,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
     const uint32_t nres = (!GRID || pl.all) ? 0u : min(*pl.rcount, (uint32_t)(2 * E));
     const int pb = pl.first ? (int)blockIdx.x : (int)blockIdx.x - pl.step_blocks;
     const long long deadline = (GRID && pl.budget) ? (long long)clock64() + pl.budget : 0;
+    bool worked = false;   // a wave always works on its first item of the launch (progress for any budget)
     for (uint32_t it = (uint32_t)(pb * nw + w); it < nnew + nres; it += (uint32_t)(pl.pend_blocks * nw)) {
         int64_t e, cc;
         int32_t rc;
@@ -1728,8 +1758,9 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
             cc = (int64_t)((uint64_t)q[2] | ((uint64_t)q[3] << 32));
             if (rc < S.reset_count[e]) continue;   // its reset has come and gone (drawn inline)
         }
-        if (deadline && (long long)clock64() > deadline) {   // out of budget: park the item unstarted / as is
+        if (deadline && worked && (long long)clock64() > deadline) {   // out of budget: park the item unstarted / as is
             if (lane == 0) {
+                atomicAdd(pl.stats + (started ? 1 : 0), 1u);
                 const uint32_t k = atomicAdd(pl.rcount_w, 1u);
                 if (k < (uint32_t)(2 * E)) {
                     uint32_t *q = pl.rlist_w + 4 * k;
@@ -1766,6 +1797,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
             ovf = P.ovf[e]; sc = P.sc[e];
             m.p = P.pos[e]; m.have1 = false; m.slid = false;
             m.key = mtw[0];
+            if (lane == 0) atomicAdd(pl.stats + 2, 1u);
             wsync();
         }
 #ifdef CN_STAMPS
@@ -1773,10 +1805,13 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
 #endif
         const int done = spawn_env<GRID>(c, c.env_offset + orow(pl.ov, e), cc, rc, pl.counter_offset, m, en, rth, ovf,
                                          sc, i0, deadline);
+        worked = true;
         const bool in1 = !m.phx && m.p > CN_MT_N;
-        write_pending(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
+        write_pending<GRID>(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
                       lane, done == N ? pl.launch_id : 0u, done);
+        if (GRID && started && done == N && lane == 0) atomicAdd(pl.stats + 3, 1u);
         if (GRID && done < N && lane == 0) {   // parked mid-way
+            atomicAdd(pl.stats + 1, 1u);
             const uint32_t k = atomicAdd(pl.rcount_w, 1u);
             if (k < (uint32_t)(2 * E)) {
                 uint32_t *q = pl.rlist_w + 4 * k;
@@ -2899,7 +2934,8 @@ struct cn_engine {
     int64_t state_bytes;
     cn_state_ptrs s;
     uint32_t *work;       // [E]
-    uint32_t *work_count; // [16]: [2..4] spawn-list counters (triple buffered)
+    uint32_t *work_count; // [16]: [2..4] spawn-list counters (triple buffered), [5..7] parked-spawn counters,
+                          // [8..11] spawn statistics (PendLaunch::stats)
     uint32_t *plist;      // [3][E] envs whose next spawn kernel A draws
     uint32_t *rlist;      // [3][2E][4] spawns parked by a launch (resumed by the next); counters work_count[5..7]
     long long spawn_budget;   // clock cycles a spawning wave works per launch before parking (0: never)
@@ -2995,6 +3031,145 @@ __global__ void __launch_bounds__(64) cn_orca_kernel(int64_t n, int A, const flo
         float rx, ry;
         const int fail_at = lp2_q(Ls[q], cnt, vmax, ox, oy, sq, rx, ry);
         if (fail_at < cnt) lp3_q(Ls[q], Ps[q], cnt, fail_at, vmax, sq, rx, ry);
+        if (sq == 0) {
+            out[4 * i] = rx; out[4 * i + 1] = ry; out[4 * i + 2] = (float)fail_at; out[4 * i + 3] = (float)cnt;
+        }
+    }
+}
+
+// cn_orca_predict_kd: ORCA.predict of simulators of any size up to CN_ORCA_MAXA agents, with RVO2's KdTree
+// (MAX_LEAF_SIZE 10) and its persisted agents_ order. One quad per simulator (16 per 64-lane workgroup):
+// lane 0 of the quad builds the tree (buildAgentTreeRecursive, which re-permutes agents_ in place) and runs
+// the query (queryAgentTreeRecursive + insertAgentNeighbor with maxNeighbors = A - 1), both sequential as
+// in RVO2 -- the plugin serves one predict per agent per env step, off the batched step path, which has its
+// own ballot-partitioned walk; then the quad builds the ORCA lines in neighbour order and runs the quad
+// linear programs of the step kernel. Oracle: cpu_ref.c:kd_build / kd_query / rvo2_agent0.
+#define CN_ORCA_MAXA 64
+struct KdNodeS { int begin, end, left, right; float minX, maxX, minY, maxY; };
+
+__device__ __forceinline__ float kd_bdist(const KdNodeS &t, float x, float y)
+{
+    const float a = (0.0f < t.minX - x) ? t.minX - x : 0.0f, b = (0.0f < x - t.maxX) ? x - t.maxX : 0.0f;
+    const float cc = (0.0f < t.minY - y) ? t.minY - y : 0.0f, d = (0.0f < y - t.maxY) ? y - t.maxY : 0.0f;
+    return a * a + b * b + cc * cc + d * d;
+}
+
+// lane-sequential KdTree build + query over X / Y [A] (LDS), perm [A] (LDS, updated in place); writes the
+// neighbours of agent 0 in insertion-sorted order to nb [A - 1] (agent ids) and returns their count
+__device__ int kd_neighbors_seq(int A, const float *X, const float *Y, uint8_t *perm, float rangeSq, uint8_t *nb)
+{
+    KdNodeS T[2 * CN_ORCA_MAXA];
+    int stk[CN_ORCA_MAXA + 2][3];
+    int sp = 0;
+    stk[sp][0] = 0; stk[sp][1] = A; stk[sp][2] = 0; ++sp;
+    while (sp > 0) {   // any order of the recursive calls gives the same tree: children own disjoint ranges
+        --sp;
+        const int begin = stk[sp][0], end = stk[sp][1], node = stk[sp][2];
+        KdNodeS t;
+        t.begin = begin; t.end = end; t.left = t.right = 0;
+        t.minX = t.maxX = X[perm[begin]];
+        t.minY = t.maxY = Y[perm[begin]];
+        for (int i = begin + 1; i < end; ++i) {
+            const float x = X[perm[i]], y = Y[perm[i]];
+            t.maxX = t.maxX < x ? x : t.maxX; t.minX = x < t.minX ? x : t.minX;
+            t.maxY = t.maxY < y ? y : t.maxY; t.minY = y < t.minY ? y : t.minY;
+        }
+        if (end - begin > 10) {
+            const bool vert = t.maxX - t.minX > t.maxY - t.minY;
+            const float split = vert ? 0.5f * (t.maxX + t.minX) : 0.5f * (t.maxY + t.minY);
+            int left = begin, right = end;
+            while (left < right) {
+                while (left < right && (vert ? X[perm[left]] : Y[perm[left]]) < split) ++left;
+                while (right > left && (vert ? X[perm[right - 1]] : Y[perm[right - 1]]) >= split) --right;
+                if (left < right) {
+                    const uint8_t s = perm[left]; perm[left] = perm[right - 1]; perm[right - 1] = s;
+                    ++left; --right;
+                }
+            }
+            if (left == begin) { ++left; ++right; }
+            t.left = node + 1;
+            t.right = node + 2 * (left - begin);
+            stk[sp][0] = left; stk[sp][1] = end; stk[sp][2] = t.right; ++sp;
+            stk[sp][0] = begin; stk[sp][1] = left; stk[sp][2] = t.left; ++sp;
+        }
+        T[node] = t;
+    }
+    // query: a node popped with distance d is walked only if d < rangeSq at that moment (the recursion tests
+    // the nearer child at once and the farther one after the nearer subtree; ties visit the right first)
+    const int maxN = A - 1;
+    float nd[CN_ORCA_MAXA];
+    int cnt = 0;
+    float dst[CN_ORCA_MAXA + 2];
+    int nst[CN_ORCA_MAXA + 2];
+    sp = 0;
+    nst[0] = 0; dst[0] = -1.0f; sp = 1;
+    const float x0 = X[0], y0 = Y[0];
+    while (sp > 0) {
+        --sp;
+        const int node = nst[sp];
+        if (!(dst[sp] < rangeSq)) continue;
+        const KdNodeS &t = T[node];
+        if (t.end - t.begin <= 10) {
+            for (int i = t.begin; i < t.end; ++i) {   // Agent::insertAgentNeighbor
+                const int a = perm[i];
+                if (a == 0) continue;
+                const float dx = x0 - X[a], dy = y0 - Y[a];
+                const float distSq = dx * dx + dy * dy;
+                if (distSq < rangeSq) {
+                    if (cnt < maxN) { nd[cnt] = distSq; nb[cnt] = (uint8_t)a; ++cnt; }
+                    int k = cnt - 1;
+                    while (k != 0 && distSq < nd[k - 1]) { nd[k] = nd[k - 1]; nb[k] = nb[k - 1]; --k; }
+                    nd[k] = distSq; nb[k] = (uint8_t)a;
+                    if (cnt == maxN) rangeSq = nd[cnt - 1];
+                }
+            }
+            continue;
+        }
+        const float dl = kd_bdist(T[t.left], x0, y0), dr = kd_bdist(T[t.right], x0, y0);
+        if (dl < dr) { nst[sp] = t.right; dst[sp] = dr; nst[sp + 1] = t.left; dst[sp + 1] = dl; }
+        else { nst[sp] = t.left; dst[sp] = dl; nst[sp + 1] = t.right; dst[sp + 1] = dr; }
+        sp += 2;
+    }
+    return cnt;
+}
+
+__global__ void __launch_bounds__(64) cn_orca_kd_kernel(int64_t n, int A, const float *__restrict__ ag,
+                                                        const float *__restrict__ self, float nd, float th, float ts,
+                                                        uint8_t *__restrict__ perm_io, float *__restrict__ out)
+{
+    __shared__ float4 Ls[16][CN_ORCA_MAXA - 1], Ps[16][CN_ORCA_MAXA - 1];
+    __shared__ float Xs[16][CN_ORCA_MAXA], Ys[16][CN_ORCA_MAXA];
+    __shared__ uint8_t Pm[16][CN_ORCA_MAXA], Nb[16][CN_ORCA_MAXA];
+    __shared__ int Cn[16];
+    const int q = threadIdx.x >> 2, sq = threadIdx.x & 3;
+    const int64_t i = (int64_t)blockIdx.x * 16 + q;
+    const bool act = i < n;
+    const float *a = ag + (act ? i : 0) * A * 5;
+    if (act)
+        for (int k = sq; k < A; k += 4) {
+            Xs[q][k] = a[k * 5]; Ys[q][k] = a[k * 5 + 1];
+            Pm[q][k] = perm_io ? perm_io[i * A + k] : (uint8_t)k;
+        }
+    wsync();
+    if (act && sq == 0) Cn[q] = A > 1 ? kd_neighbors_seq(A, Xs[q], Ys[q], Pm[q], nd * nd, Nb[q]) : 0;
+    wsync();
+    if (act) {
+        const int cnt = Cn[q];
+        const float invTH = fdiv(1.0f, th), invTS = fdiv(1.0f, ts);
+        for (int k = sq; k < cnt; k += 4) {
+            const float *o = a + Nb[q][k] * 5;
+            Ls[q][k] = orca_line(a[0], a[1], a[2], a[3], a[4], o[0], o[1], o[2], o[3], o[4], invTH, invTS);
+        }
+        if (perm_io)
+            for (int k = sq; k < A; k += 4) perm_io[i * A + k] = Pm[q][k];
+    }
+    wsync();
+    if (act) {
+        const int cnt = Cn[q];
+        const float vmax = self[3 * i], ox = self[3 * i + 1], oy = self[3 * i + 2];
+        float rx, ry;
+        const int fail_at = lp2_q<uint64_t>(Ls[q], cnt, vmax, ox, oy, sq, rx, ry);
+        if (fail_at < cnt) lp3_q<uint64_t>(Ls[q], Ps[q], cnt, fail_at, vmax, sq, rx, ry);
         if (sq == 0) {
             out[4 * i] = rx; out[4 * i + 1] = ry; out[4 * i + 2] = (float)fail_at; out[4 * i + 3] = (float)cnt;
         }
@@ -3368,6 +3543,7 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     a.o.case_size = g->case_size;
     a.o.ov.row = g->rows; a.o.ov.NS = g->NS;
     a.pend = g->pend; a.E = g->E; a.counter_offset = g->counter_offset;
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_reset_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
     HIPCHK(hipGetLastError());
     g->pend_all = 1;   // every env starts a new episode: draw all next spawns in the next kernel A
@@ -3391,7 +3567,10 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
             if (k > 0) { sk = g->gstream[k]; HIPCHK(hipStreamWaitEvent(sk, g->gev[0], 0)); }
             const int rc = cn_step(g->grp[k], (void *)sk, actions, robot_node, temporal, spatial, reward, done, event,
                                    info, ep_return, ep_len);
-            if (rc) return rc;
+            if (rc) {   // join the groups already forked, so no side-stream work outlives the caller's order
+                for (int j = 1; j < k; ++j) (void)hipStreamWaitEvent(st, g->gev[j], 0);
+                return rc;
+            }
             if (k > 0) HIPCHK(hipEventRecord(g->gev[k], sk));
         }
         for (int k = 1; k < g->ngroups; ++k) HIPCHK(hipStreamWaitEvent(st, g->gev[k], 0));
@@ -3410,6 +3589,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.pend.rlist = g->rlist + (int64_t)kr * 4 * (2 * (int64_t)g->E + 64); a.pend.rcount = g->work_count + 5 + kr;
     a.pend.rlist_w = g->rlist + (int64_t)kw * 4 * (2 * (int64_t)g->E + 64); a.pend.rcount_w = g->work_count + 5 + kw;
     a.pend.budget = g->spawn_budget;
+    a.pend.stats = g->work_count + 8;
     a.pend.launch_id = (uint32_t)(g->nstep % 0x7ffffffeu) + 1u;   // nonzero, differs from the neighbours'
     const int blocks = (g->E + g->plan.EPB - 1) / g->plan.EPB;
     a.pend.P = g->pend; a.pend.list = g->plist + (int64_t)kr * (g->E + 64); a.pend.count = g->work_count + 2 + kr;
@@ -3430,6 +3610,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
         cn_step_kernel<false, false, false>, cn_step_kernel<false, false, true>, cn_step_kernel<false, true, false>,
         cn_step_kernel<false, true, true>,   cn_step_kernel<true, false, false>,  cn_step_kernel<true, false, true>,
         cn_step_kernel<true, true, false>,   cn_step_kernel<true, true, true>};
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(kern[variant], dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
     HIPCHK(hipGetLastError());
     if (prof && ++g->prof_n == g->prof_cap) HIPCHK(hipEventRecord(g->ev[1], st));
@@ -3508,6 +3689,32 @@ int cn_debug_stamps(unsigned long long *a, unsigned long long *b)
 }
 #endif
 
+int cn_debug_set_spawn_budget(cn_engine *g, long long cycles)
+{
+    if (!g || cycles < 0) return set_err(CN_EINVAL, "cn_debug_set_spawn_budget: engine and cycles >= 0 required");
+    for (int k = 0; k < g->ngroups; ++k) cn_debug_set_spawn_budget(g->grp[k], cycles);
+    if (!g->ngroups && g->plan.kd) g->spawn_budget = cycles;   // parking exists on the kd-tree path only
+    return CN_OK;
+}
+
+int cn_debug_spawn_stats(cn_engine *g, uint32_t *out)
+{
+    if (!g || !out) return set_err(CN_EINVAL, "null argument");
+    for (int j = 0; j < 4; ++j) out[j] = 0;
+    if (g->ngroups) {
+        for (int k = 0; k < g->ngroups; ++k) {
+            uint32_t v[4];
+            const int rc = cn_debug_spawn_stats(g->grp[k], v);
+            if (rc) return rc;
+            for (int j = 0; j < 4; ++j) out[j] += v[j];
+        }
+        return CN_OK;
+    }
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpy(out, g->work_count + 8, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return CN_OK;
+}
+
 int cn_lidar_obs(cn_engine *g, void *stream, const uint8_t *reset_mask, int enable, int beams, double max_range,
                  double robot_radius, float *lidar, float *obs)
 {
@@ -3515,6 +3722,7 @@ int cn_lidar_obs(cn_engine *g, void *stream, const uint8_t *reset_mask, int enab
     if (g->ngroups) return set_err(CN_EUNSUPPORTED, "cn_lidar_obs: not on a mixed engine");
     if (beams < 2 || beams > 4096 || !(max_range > 0) || !lidar || !obs)
         return set_err(CN_EINVAL, "cn_lidar_obs: beams in [2, 4096], max_range > 0 and buffers required");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_lidar_obs_kernel, dim3((unsigned)((g->E + 3) / 4)), dim3(256), 0, (hipStream_t)stream, g->s,
                        g->E, g->N, 0.5 * g->c.square_width, reset_mask, enable, beams, max_range, robot_radius,
                        lidar, obs);
@@ -3527,6 +3735,7 @@ int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, cons
 {
     if (n <= 0 || !px || !py || !r || !qx || !qy || !out) return set_err(CN_EINVAL, "cn_debug_disc_quad: n > 0 and buffers required");
     HIPCHK(circ_table_init());
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_disc_quad_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, n, mode,
                        px, py, r, qx, qy, out);
     HIPCHK(hipGetLastError());
@@ -3536,6 +3745,7 @@ int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, cons
 int cn_debug_copy64(void *stream, int64_t n, int seg, const double *src, double *dst)
 {
     if (n <= 0 || seg < 1 || seg > 64 || !src || !dst) return set_err(CN_EINVAL, "cn_debug_copy64: n > 0, 1 <= seg <= 64");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_copy64_kernel, dim3((unsigned)((n + seg - 1) / seg)), dim3(64), 0, (hipStream_t)stream, n, seg,
                        src, dst);
     HIPCHK(hipGetLastError());
@@ -3547,8 +3757,21 @@ int cn_debug_orca(void *stream, int64_t n, int A, const float *agents, const flo
 {
     if (n <= 0 || !agents || !self || !out) return set_err(CN_EINVAL, "cn_debug_orca: n > 0 and buffers required");
     if (A < 1 || A > 10) return set_err(CN_EUNSUPPORTED, "cn_debug_orca: 1 <= A <= 10 (the quad path)");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_orca_kernel, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, (hipStream_t)stream, n, A,
                        agents, self, neighbor_dist, time_horizon, time_step, out);
+    HIPCHK(hipGetLastError());
+    return CN_OK;
+}
+
+int cn_orca_predict_kd(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
+                       float time_horizon, float time_step, uint8_t *perm, float *out)
+{
+    if (n <= 0 || !agents || !self || !out) return set_err(CN_EINVAL, "cn_orca_predict_kd: n > 0 and buffers required");
+    if (A < 1 || A > CN_ORCA_MAXA) return set_err(CN_EUNSUPPORTED, "cn_orca_predict_kd: 1 <= A <= 64");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
+    hipLaunchKernelGGL(cn_orca_kd_kernel, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, (hipStream_t)stream, n, A,
+                       agents, self, neighbor_dist, time_horizon, time_step, perm, out);
     HIPCHK(hipGetLastError());
     return CN_OK;
 }
@@ -3556,6 +3779,8 @@ int cn_debug_orca(void *stream, int64_t n, int A, const float *agents, const flo
 int cn_orca_predict(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
                     float time_horizon, float time_step, float *out)
 {
+    if (A > 10)   // a fresh simulator per call: identity KdTree order
+        return cn_orca_predict_kd(stream, n, A, agents, self, neighbor_dist, time_horizon, time_step, nullptr, out);
     return cn_debug_orca(stream, n, A, agents, self, neighbor_dist, time_horizon, time_step, out);
 }
 
@@ -3564,6 +3789,7 @@ int cn_social_force_predict(void *stream, int64_t n, int M, const double *self, 
 {
     if (n <= 0 || M < 0 || M > 64 || !self || (M && !others) || !out)
         return set_err(CN_EINVAL, "cn_social_force_predict: n > 0, 0 <= M <= 64 and buffers required");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_sf_predict_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, n, M,
                        self, others, A, B, KI, time_step, out);
     HIPCHK(hipGetLastError());
@@ -3578,6 +3804,7 @@ int cn_edge_features(void *stream, int64_t E, int N, const float *robot_node, co
     if (E <= 0 || N <= 0) return set_err(CN_EINVAL, "E, N must be > 0");
     const int64_t threads = E * (N + 2) * 16;
     const int64_t blocks = (threads + 255) / 256;
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_edge_features_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, E, N,
                        robot_node, temporal_edges, spatial_edges, Wt, bt, Ws, bs, Wr, br, Wn, bn, temporal_embed,
                        spatial_embed, node_embed);

@@ -325,6 +325,7 @@ int cn_gru_fwd_step_scatter(void *stream, int64_t B, int H, const float *gi, con
     if (B * (H / 4) > (int64_t)0xffffffff * 256) return cn_set_error(CN_EINVAL, "cn_gru_fwd_step: B too large");
     if (h_out2 && (g2 <= 0 || ld2 < g2 * H || (ld2 & 3) || ((uintptr_t)h_out2 & 15)))
         return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_scatter: g2 > 0, ld2 >= g2 * H, ld2 % 4 == 0, 16-byte aligned h_out2");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_gru_fwd_kernel, dim3(grid_for(B, H)), dim3(256), 0, (hipStream_t)stream, B, H, gi, gh,
                        hm, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2);
     hipError_t e = hipGetLastError();
@@ -337,14 +338,18 @@ int cn_gru_fwd_fused(void *stream, int64_t B, int H, const float *gi, const floa
 {
     if (B <= 0 || H <= 0 || H % GF_BU) return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: B > 0 and H % 32 == 0 required");
     if (!gi || !hm || !w_hh || !b_hh || !h_out) return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: null operand");
-    if ((((uintptr_t)hm) | ((uintptr_t)w_hh)) & 15)
-        return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: hm and w_hh must be 16-byte aligned");
+    // every operand the kernel touches with 16-byte vectors (float4 loads of hm, w_hh, gi, b_hh; float4 stores
+    // of h_out, hm_next, save); h_out2 is checked below
+    if ((((uintptr_t)hm) | ((uintptr_t)w_hh) | ((uintptr_t)gi) | ((uintptr_t)b_hh) | ((uintptr_t)h_out) |
+         ((uintptr_t)hm_next) | ((uintptr_t)save)) & 15)
+        return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: hm, w_hh, gi, b_hh, h_out, hm_next and save must be 16-byte aligned");
     if (h_out2 && (g2 <= 0 || ld2 < g2 * H))
         return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: g2 > 0 and ld2 >= g2 * H required");
     const int64_t rt = (B + GF_BM - 1) / GF_BM;
     const int ut = H / GF_BU;
     const int64_t grid = (rt + 7) / 8 * 8 * ut;
     if (grid > 0x7fffffff) return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: B too large");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_gru_fused_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, B, H, (int)rt, ut,
                        gi, hm, w_hh, b_hh, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2);
     hipError_t e = hipGetLastError();
@@ -357,6 +362,7 @@ int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_n
     if (B <= 0 || H <= 0 || (H & 3)) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step: B > 0 and H % 4 == 0 required");
     if (!acc || !save || !hm || !dgi || !dgh) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step: null operand");
     if (B * (H / 4) > (int64_t)0xffffffff * 256) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step: B too large");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_gru_bwd_kernel, dim3(grid_for(B, H)), dim3(256), 0, (hipStream_t)stream, B, H, acc,
                        m_next, dout, save, hm, dgi, dgh);
     hipError_t e = hipGetLastError();
@@ -428,6 +434,7 @@ int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, con
 {
     if (R <= 0 || N <= 0 || H <= 0 || (H & 3)) return cn_set_error(CN_EINVAL, "cn_attn_pool_fwd: bad shape");
     if (!hs || !attn || !out) return cn_set_error(CN_EINVAL, "cn_attn_pool_fwd: null operand");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_attn_pool_fwd_kernel, dim3(grid_for(R, H)), dim3(256), 0, (hipStream_t)stream, R, N, H, hs,
                        attn, out);
     hipError_t e = hipGetLastError();
@@ -441,6 +448,7 @@ int cn_attn_pool_bwd(void *stream, int64_t R, int N, int H, const float *hs, con
         return cn_set_error(CN_EINVAL, "cn_attn_pool_bwd: H must be 64, 128 or 256");
     if (!hs || !attn || !dout || !dhs || !dattn) return cn_set_error(CN_EINVAL, "cn_attn_pool_bwd: null operand");
     const unsigned grid = grid_for(R, H);
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     if (H == 256)
         hipLaunchKernelGGL(cn_attn_pool_bwd_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, hs, attn,
                            dout, dhs, dattn);

@@ -143,6 +143,18 @@ class CrowdNavEngine:
         with self.torch.cuda.device(self.device):
             _lib.check(_lib.lib().cn_set_state(self._h, self._stream(), blob.ctypes.data_as(ctypes.c_void_p), 1))
 
+    def set_spawn_budget(self, cycles):
+        """Test hook (cn_debug_set_spawn_budget): clock cycles a kd-tree-path spawning wave works per launch
+        before it parks its spawn (default 600000; 0 = never). Results do not depend on it."""
+        _lib.check(_lib.lib().cn_debug_set_spawn_budget(self._h, int(cycles)))
+
+    def spawn_stats(self):
+        """Cumulative kd-tree-path spawn counters (cn_debug_spawn_stats; synchronises): parked before
+        starting, parked mid-way, resumed, completed by a resume."""
+        out = (ctypes.c_uint32 * 4)()
+        _lib.check(_lib.lib().cn_debug_spawn_stats(self._h, out))
+        return dict(zip(("parked_unstarted", "parked_midway", "resumed", "completed_on_resume"), list(out)))
+
     def close(self):
         if getattr(self, "_h", None) is not None:
             _lib.lib().cn_destroy(self._h)

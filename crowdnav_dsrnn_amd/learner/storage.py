@@ -28,18 +28,26 @@ class CompactSteps:
             raise IndexError("step %d out of range for %d steps" % (i, self.T))
         return 0 if i in (0, -(self.T + 1)) else 1
 
+    @staticmethod
+    def _is_step(i):
+        """A single step index: a Python / numpy integer or a 0-dim integer tensor (anything with
+        __index__ that is not a slice or a multi-element tensor)."""
+        if isinstance(i, torch.Tensor):
+            return i.dim() == 0 and not i.is_floating_point() and not i.is_complex() and i.dtype != torch.bool
+        return isinstance(i, int) or (hasattr(i, "__index__") and not isinstance(i, slice))
+
     def __getitem__(self, i):
-        if isinstance(i, int) or (hasattr(i, "__index__") and not isinstance(i, (slice, torch.Tensor))):
+        if self._is_step(i):
             return self.t[self._slot(i)]
         return self.t[i]
 
-    def __setitem__(self, i, v):
-        if isinstance(i, int):
+    def __setitem__(self, i, v):   # same step mapping as __getitem__ (numpy / tensor scalars included)
+        if self._is_step(i):
             self.t[self._slot(i)] = v
         else:
             self.t[i] = v
 
-    def __len__(self):
+    def __len__(self):   # the step count it stands for; .shape / .size() are the 2-slot tensor's own
         return self.T + 1
 
     def to(self, *a, **kw):

@@ -68,6 +68,9 @@ def _torch_stream():
     return torch, dev, ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
+MAX_ORCA_AGENTS = 64   # cn_orca_predict_kd's simulator size limit (include/crowdnav.h)
+
+
 class Policy:
     """crowd_nav/policy/policy.py:5-19 (attributes the env sets: time_step, phase, env, ...)."""
 
@@ -99,15 +102,18 @@ class ORCA(Policy):
         self.max_neighbors = None
         self.radius = None
         self.max_speed = 1
-        self.sim = None   # frozen simulator parameters: (agent count, radii f32 [A], self max speed f32)
+        # the simulator's state that outlives a predict (orca.py:85-115): agent count, frozen radii f32 [A],
+        # self max speed f32, and RVO2's KdTree agent order (KdTree::agents_, re-permuted by every doStep's
+        # tree build; it decides the order of equally distant neighbours when A > 10)
+        self.sim = None
 
     def _frame(self, state):
         """float32 agents [A][5] (px, py, vx, vy, frozen radius) and [maxSpeed, pref.x, pref.y] of agent 0."""
         s, hs = state.self_state, state.human_states
         A = len(hs) + 1
-        if A > 10:
-            raise UnsupportedConfig("ORCA.predict: %d agents per simulator (the GPU predict serves <= 10; the "
-                                    "step kernel's kd-tree path serves more inside cn_step)" % A)
+        if A > MAX_ORCA_AGENTS:
+            raise UnsupportedConfig("ORCA.predict: %d agents per simulator (the GPU predict serves <= %d)"
+                                    % (A, MAX_ORCA_AGENTS))
         self.max_neighbors = len(hs)
         self.radius = s.radius
         if self.sim is not None and self.sim[0] != A:   # orca.py:85-90
@@ -115,7 +121,7 @@ class ORCA(Policy):
         if self.sim is None:                            # orca.py:91-109: parameters frozen at creation
             safety = self.config.orca.safety_space
             radii = np.array([s.radius + 0.01 + safety] + [h.radius + 0.01 + safety for h in hs], np.float32)
-            self.sim = (A, radii, np.float32(s.v_pref))
+            self.sim = (A, radii, np.float32(s.v_pref), np.arange(A, dtype=np.uint8))
         ag = np.zeros((A, 5), np.float32)
         ag[0, :4] = (s.px, s.py, s.vx, s.vy)
         for k, h in enumerate(hs):
@@ -196,8 +202,17 @@ def predict_batch(policies, states):
         res = torch.zeros((len(idx), 4), dtype=torch.float32, device=dev)
         c = policies[idx[0]].config
         ts = policies[idx[0]].time_step or c.env.time_step
-        _lib.check(L.cn_orca_predict(st, len(idx), A, ag.data_ptr(), sf.data_ptr(), float(c.orca.neighbor_dist),
-                                     float(c.orca.time_horizon), float(ts), res.data_ptr()))
+        if A > 10:   # KdTree path: each simulator's persisted agent order goes in and comes back re-permuted
+            perm = torch.from_numpy(np.stack([policies[i].sim[3] for i in idx])).to(dev)
+            _lib.check(L.cn_orca_predict_kd(st, len(idx), A, ag.data_ptr(), sf.data_ptr(),
+                                            float(c.orca.neighbor_dist), float(c.orca.time_horizon), float(ts),
+                                            perm.data_ptr(), res.data_ptr()))
+            pn = perm.cpu().numpy()
+            for k, i in enumerate(idx):
+                policies[i].sim[3][:] = pn[k]
+        else:
+            _lib.check(L.cn_orca_predict(st, len(idx), A, ag.data_ptr(), sf.data_ptr(), float(c.orca.neighbor_dist),
+                                         float(c.orca.time_horizon), float(ts), res.data_ptr()))
         r = res.cpu().numpy()
         for k, i in enumerate(idx):
             out[i] = ActionXY(float(r[k, 0]), float(r[k, 1]))

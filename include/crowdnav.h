@@ -21,7 +21,11 @@
  *                   HumanNodeRNN.encoder_linear+ReLU (srnn_model.py:160-161)
  *   cn_gru_fwd_step / cn_gru_bwd_step ⟵ one time step of the mask-segmented GRU
  *                   (srnn_model.py:52-104 RNNBase._forward_gru, torch nn.GRU cell math) and its gradient;
- *                   the GEMMs around them (x W_ih^T, hm W_hh^T, dgh W_hh) are library GEMMs
+ *                   cn_gru_fwd_fused runs the recurrent GEMM hm W_hh^T on the f32 MFMA with the gates in its
+ *                   epilogue (the forward's per-step kernel); x W_ih^T over all steps and the backward's
+ *                   dgh W_hh remain library GEMMs
+ *   cn_orca_predict / cn_orca_predict_kd / cn_social_force_predict ⟵ the agent policy plugin
+ *                   policy_factory[name](config).predict(JointState) (crowd_nav/policy/policy_factory.py:1-17)
  *   cn_lidar_obs     ⟵ CrowdSimDict.generate_ob's 'convgru' observation (crowd_sim_dict.py:96-101) with
  *                   LidarSensor.sensor_spin (crowd_sim/envs/utils/lidarv2.py:398-427) evaluated at reset
  *   cn_attn_pool_fwd / cn_attn_pool_bwd ⟵ EdgeAttention's weighted sum of the spatial edge states
@@ -227,8 +231,8 @@ int cn_gru_fwd_step_scatter(void *stream, int64_t B, int H, const float *gi, con
 
 /* Fused step: the recurrent GEMM gh = hm W_hh^T + b_hh (w_hh [3H][H] row-major, as nn.GRU's weight_hh_l0;
  * b_hh [3H]) on the f32 matrix cores with cn_gru_fwd_step_scatter's gate epilogue, so gh never leaves the
- * chip. Same outputs and arguments as cn_gru_fwd_step_scatter otherwise; H % 32 == 0, hm and w_hh
- * 16-byte aligned with rows of H contiguous. Replaces torch.addmm + cn_gru_fwd_step per time step of
+ * chip. Same outputs and arguments as cn_gru_fwd_step_scatter otherwise; H % 32 == 0; hm, w_hh, gi, b_hh,
+ * h_out, hm_next and save 16-byte aligned (float4 accesses) with rows contiguous; CN_EINVAL otherwise. Replaces torch.addmm + cn_gru_fwd_step per time step of
  * srnn_model.py:52-104's nn.GRU. */
 int cn_gru_fwd_fused(void *stream, int64_t B, int H, const float *gi, const float *hm, const float *w_hh,
                      const float *b_hh, const float *m_next, float *h_out, float *hm_next, float *save, float *h_out2,
@@ -270,25 +274,42 @@ int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, cons
 int cn_debug_orca(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
                   float time_horizon, float time_step, float *out);
 
-/* Profiler calibration hook (MI355X_MICROARCH.md § HBM: FETCH_SIZE / WRITE_SIZE are calibrated only for
- * 16-B-per-lane streams): dst[k] = src[k] over n doubles with the step kernel's access shape, one 8-B load
- * and store per lane, in segments of `seg` consecutive doubles per 64-lane wave (seg = 64: a field of the
- * per-human SoA arrays; seg = 6: a per-env field of one workgroup). tools/calib_pmc.py reads the
- * counters of known byte counts through it. */
 /* Agent policy plugin (replaces policy_factory[name](config).predict(JointState),
  * crowd_nav/policy/policy_factory.py:1-17; host side crowdnav_dsrnn_amd/policy_factory.py).
- * cn_orca_predict: ORCA.predict (crowd_nav/policy/orca.py:64-139) of n independent simulators of A <= 10
+ * cn_orca_predict: ORCA.predict (crowd_nav/policy/orca.py:64-139) of n independent simulators of A <= 64
  *   agents, arguments and outputs as cn_debug_orca (the caller keeps the simulator's frozen radii and max
- *   speed, orca.py:85-115).
+ *   speed, orca.py:85-115). A > 10 runs cn_orca_predict_kd with a fresh simulator's (identity) KdTree order.
+ * cn_orca_predict_kd: the same for simulators of A <= 64 agents through RVO2's KdTree (MAX_LEAF_SIZE 10),
+ *   whose build re-permutes the simulator's persisted agent order (KdTree::agents_): perm [n][A] uint8 holds
+ *   each simulator's order on entry (identity for a simulator created by this predict) and the re-permuted
+ *   order on return, so a caller that keeps one simulator across predicts (orca.py:85-90: the simulator
+ *   lives until the agent count changes) passes it back next time. perm = NULL: identity, not written.
+ *   Caller side: crowd_sim.py:1121-1161 passes N-1 humans (+ the robot when robot.visible), i.e. A = N or N+1.
  * cn_social_force_predict: SOCIAL_FORCE.predict (crowd_nav/policy/social_force.py:11-66) of n agents,
  *   float64: self [n][9] = FullState (px, py, vx, vy, radius, gx, gy, v_pref, theta), others [n][M][5] =
  *   ObservableState (px, py, vx, vy, radius), A / B / KI = config.sf, time_step = config.env.time_step;
  *   out [n][2] = the ActionXY (vx, vy). Device pointers, stream-ordered. */
 int cn_orca_predict(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
                     float time_horizon, float time_step, float *out);
+int cn_orca_predict_kd(void *stream, int64_t n, int A, const float *agents, const float *self, float neighbor_dist,
+                       float time_horizon, float time_step, uint8_t *perm, float *out);
 int cn_social_force_predict(void *stream, int64_t n, int M, const double *self, const double *others, double A,
                             double B, double KI, double time_step, double *out);
 
+/* Test hooks of the kd-tree path's resumable spawns (the spawn waves that draw upcoming episodes park a
+ * crowded spawn between two humans once a wave has worked `cycles` clock cycles in a launch, and a later
+ * launch resumes it; default 600000, 0 = never park; no effect on the quad path, which never parks).
+ * cn_debug_spawn_stats: cumulative counts since cn_create [4] = spawns parked before they started, parked
+ * mid-way, resumed, completed by a resume (synchronises the device). Results do not depend on the budget:
+ * tests/test_gpu_parity.py forces parking after every human and compares with the oracle. */
+int cn_debug_set_spawn_budget(cn_engine *eng, long long cycles);
+int cn_debug_spawn_stats(cn_engine *eng, uint32_t *out);
+
+/* Profiler calibration hook (MI355X_MICROARCH.md § HBM: FETCH_SIZE / WRITE_SIZE are calibrated only for
+ * 16-B-per-lane streams): dst[k] = src[k] over n doubles with the step kernel's access shape, one 8-B load
+ * and store per lane, in segments of `seg` consecutive doubles per 64-lane wave (seg = 64: a field of the
+ * per-human SoA arrays; seg = 6: a per-env field of one workgroup). tools/calib_pmc.py reads the
+ * counters of known byte counts through it. */
 int cn_debug_copy64(void *stream, int64_t n, int seg, const double *src, double *dst);
 
 /* out[r][h] = sum_n hs[r][n][h] * attn[r][n]; hs [R][N][H], attn [R][N], out [R][H]; H % 4 == 0. */

@@ -220,6 +220,88 @@ def test_gpu_free_running_matches_oracle_short_horizon(gpu, oracle, rng, shape):
         assert not errs, errs
 
 
+def _free_run_exact(ref, g, cfg, steps, kind, seed):
+    """Free-running GPU vs oracle with identical actions: done / event exact, rewards 1e-5 every step."""
+    rng = np.random.RandomState(seed)
+    for t in range(steps):
+        a = (rng.uniform(-0.1, 0.1, (cfg.num_envs, 2)) if kind == "unicycle"
+             else rng.normal(0, 0.5, (cfg.num_envs, 2))).astype(np.float32)
+        r1, r2 = ref.step(a), g.step(a)
+        np.testing.assert_array_equal(r2[2], r1[2], err_msg="done t=%d" % t)
+        np.testing.assert_array_equal(r2[3], r1[3], err_msg="event t=%d" % t)
+        np.testing.assert_allclose(r2[1], r1[1], atol=1e-5, rtol=0, err_msg="reward t=%d" % t)
+
+
+def test_gpu_forced_spawn_parking_matches_oracle(gpu, oracle):
+    """The kd-tree path's resumable spawns under a 1-cycle budget: every spawning wave parks its spawn after
+    each human (at least one human per launch), so every upcoming episode is drawn over ~25 launches through
+    the park / resume machinery (stored MT block and stream position, the robot and the humans so far,
+    overflow count, scenario, Philox key), and resets that find their spawn unfinished draw inline. The
+    rollout must equal the oracle exactly (done / event every step, state and every stream at the end), and
+    the counters must show spawns parked mid-way, resumed and completed by a resume."""
+    for rngmode in ("mt19937", "philox"):
+        # 96 envs: fewer pending items than the 256 spawning waves, so every parked spawn is resumed by the
+        # next launch and completes ~25 launches after it started
+        cfg = _cfg(25, "holonomic", "square_crossing", E=96, fov=1.0, env__rng=rngmode)
+        ref, g = oracle.RefEngine(cfg), gpu(cfg)
+        g.eng.set_spawn_budget(1)
+        ref.reset()
+        g.reset()
+        _free_run_exact(ref, g, cfg, 100, "holonomic", 17)
+        rs, gs = ref.get_state(), g.get_state()
+        d = {"post_" + n: np.asarray(getattr(rs, n)) for n, _, _ in abi.STATE_FIELDS if n != "mt"}
+        d["post_mt_crc"] = H.mt_crc(rs)
+        errs = H.compare_state(gs, d, "post_", tol=1e-5)
+        assert not errs, errs
+        st = g.eng.spawn_stats()
+        assert st["parked_midway"] > 1000 and st["resumed"] > 1000 and st["completed_on_resume"] > 50, (rngmode, st)
+
+
+def test_gpu_full_size_c3_free_running(gpu, oracle):
+    """BASELINE config 3 at its full size (4096 envs x 25 humans, square_crossing, robot / human FOV pi,
+    holonomic: the kd-tree path, the bench's --workload c3) for 400 free-running steps: the first 40 steps
+    identical to the oracle, then finite outputs, done exactly where the event is terminal, Monitor lengths
+    within the time limit, each env's reset count = 1 + its episodes ended, episode counts / mean return
+    within 2 % of the oracle's over the 400 steps, and the spawn counters show spawns parked and resumed at
+    the default budget (the crowded spawns of this workload outlast it)."""
+    E = 4096
+    cfg = _cfg(25, "holonomic", "square_crossing", E=E, fov=1.0)
+    oracle.lib().cnref_set_threads(min(16, os.cpu_count() or 1))
+    ref, g = oracle.RefEngine(cfg), gpu(cfg)
+    ref.reset()
+    g.reset()
+    rc0 = np.asarray(g.get_state().reset_count).copy()
+    rng = np.random.RandomState(5)
+    term = np.isin(np.arange(5), [abi.EV_COLLISION, abi.EV_REACHGOAL, abi.EV_TIMEOUT])
+    n_ep, ret = [0, 0], [0.0, 0.0]
+    ended = np.zeros(E, np.int64)
+    tmax = int(round(cfg.time_limit / cfg.time_step)) + 1
+    for t in range(400):
+        a = rng.normal(0, 0.5, (E, 2)).astype(np.float32)
+        r1, r2 = ref.step(a), g.step(a)
+        if t < 40:
+            np.testing.assert_array_equal(r2[2], r1[2], err_msg="done t=%d" % t)
+            np.testing.assert_array_equal(r2[3], r1[3], err_msg="event t=%d" % t)
+            np.testing.assert_allclose(r2[1], r1[1], atol=1e-5, rtol=0, err_msg="reward t=%d" % t)
+        for k in r2[0]:
+            assert np.isfinite(r2[0][k]).all(), (k, t)
+        assert np.isfinite(r2[1]).all()
+        d = r2[2].astype(bool)
+        np.testing.assert_array_equal(d, term[r2[3]], err_msg="done vs event t=%d" % t)
+        assert (r2[6][d] >= 1).all() and (r2[6][d] <= tmax).all(), t
+        ended += d
+        for k, r in enumerate((r1, r2)):
+            dd = r[2].astype(bool)
+            n_ep[k] += int(dd.sum())
+            ret[k] += float(r[5][dd].sum())
+    np.testing.assert_array_equal(np.asarray(g.get_state().reset_count) - rc0, ended)
+    assert n_ep[1] > 1000, n_ep
+    assert abs(n_ep[1] - n_ep[0]) <= 0.02 * n_ep[0], n_ep
+    assert abs(ret[1] / n_ep[1] - ret[0] / n_ep[0]) <= 0.02 * abs(ret[0] / n_ep[0]) + 0.05, (ret, n_ep)
+    st = g.eng.spawn_stats()
+    assert st["parked_midway"] > 0 and st["resumed"] > 0 and st["completed_on_resume"] > 0, st
+
+
 def test_gpu_full_size_c2_free_running(gpu, oracle):
     """BASELINE config 2 at its full size (4096 envs x 10 humans, the bench workload) for 400 free-running
     steps: the first 50 steps identical to the oracle (done / event exact, rewards 1e-5; the oracle on all

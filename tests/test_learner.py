@@ -301,3 +301,24 @@ def test_rollout_trainer_matches_reference_train_loop():
     tr.update()
     assert abs(agent.optimizer.param_groups[0]["lr"] - c.training.lr * 0.75) < 1e-12
     envs.close()
+
+
+def test_compact_steps_index_types():
+    """CompactSteps maps every integer-like step (int, numpy integer, 0-dim integer tensor) to the same slot
+    for reads AND writes: step 0 / -(T+1) -> slot 0, any other step -> slot 1."""
+    import numpy as np
+    import torch
+
+    from crowdnav_dsrnn_amd.learner.storage import CompactSteps
+
+    T = 5
+    c = CompactSteps(torch.zeros(2, 3), T)
+    for k, idx in enumerate((3, np.int64(4), torch.tensor(2), np.int32(T))):
+        c[idx] = float(k + 1)
+        assert float(c.t[1, 0]) == k + 1 and float(c.t[0, 0]) == 0.0
+        assert float(c[idx][0]) == k + 1
+    c[np.int64(0)] = 7.0
+    assert float(c.t[0, 0]) == 7.0 and float(c[-(T + 1)][0]) == 7.0
+    with pytest.raises(IndexError):
+        c[np.int64(T + 1)] = 1.0
+    assert len(c) == T + 1 and c.shape[0] == 2
