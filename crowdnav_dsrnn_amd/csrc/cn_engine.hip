@@ -624,6 +624,145 @@ __device__ __forceinline__ void lp3_q(const float4 *Lb, float4 *Pb, int n, int b
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// The same linear programs with the lines in REGISTERS (quad path, <= 4 * NU lines): lane s of the quad
+// holds lines s, s+4, ..., s+4(NU-1) (R[u] = line s + 4u) and line i reaches the whole quad by a DPP
+// quad_perm broadcast from lane i & 3 -- the loops over lines are unrolled, so every broadcast has a
+// compile-time source lane and no LDS round trip sits on the linear programs' dependent chain. Same
+// operations in the same order as lp1_q / lp2_q / lp3_q, so the same bits.
+// ------------------------------------------------------------------------------------------------
+template <int T>
+__device__ __forceinline__ float qbc(float x)   // quad_perm(T, T, T, T): lane T of the quad to all four
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), T * 0x55, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float4 qbc4(const float4 v, int t)   // t folds to a constant once unrolled
+{
+    switch (t & 3) {
+    case 0: return make_float4(qbc<0>(v.x), qbc<0>(v.y), qbc<0>(v.z), qbc<0>(v.w));
+    case 1: return make_float4(qbc<1>(v.x), qbc<1>(v.y), qbc<1>(v.z), qbc<1>(v.w));
+    case 2: return make_float4(qbc<2>(v.x), qbc<2>(v.y), qbc<2>(v.z), qbc<2>(v.w));
+    default: return make_float4(qbc<3>(v.x), qbc<3>(v.y), qbc<3>(v.z), qbc<3>(v.w));
+    }
+}
+__device__ __forceinline__ float qbcf(const float v, int t)
+{
+    switch (t & 3) {
+    case 0: return qbc<0>(v);
+    case 1: return qbc<1>(v);
+    case 2: return qbc<2>(v);
+    default: return qbc<3>(v);
+    }
+}
+
+// linearProgram1 on line `no` (= ln, already broadcast) against the valid (vmask) lines j < no of R
+template <int NU>
+__device__ __forceinline__ bool lp1_r(const float4 (&R)[NU], uint32_t vmask, int no, const float4 ln, float radius,
+                                      int s, float &tL, float &tR)
+{
+    const float dot = ln.x * ln.z + ln.y * ln.w;
+    const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
+    const float sd = fsqrt(disc);
+    float ptl = -INFINITY, ptr = INFINITY;
+    int pf = 0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int j = s + 4 * u;
+        if (j < no && ((vmask >> j) & 1u)) {
+            const float4 li = R[u];
+            const float den = det2(ln.z, ln.w, li.z, li.w);
+            const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
+            const bool par = fabsf(den) <= RVO_EPSILON;
+            if (par && num < 0.0f) pf = 1;
+            const float t = fdiv(num, den);
+            if (!par && den >= 0.0f && t < ptr) ptr = t;
+            if (!par && !(den >= 0.0f) && ptl < t) ptl = t;
+        }
+    }
+    ptr = quad_min(ptr);
+    ptl = quad_max(ptl);
+    pf = quad_or(pf);
+    float tr = -dot + sd, tl = -dot - sd;
+    tr = ptr < tr ? ptr : tr;
+    tl = tl < ptl ? ptl : tl;
+    tL = tl; tR = tr;
+    return !(disc < 0.0f || pf || tl > tr);
+}
+
+// linearProgram2 (optimize closest to (ox, oy)) over the n lines of R; returns the failing line or n
+template <int NU>
+__device__ __forceinline__ int lp2_r(const float4 (&R)[NU], int n, float radius, float ox, float oy, int s, float &rx,
+                                     float &ry)
+{
+    if (ox * ox + oy * oy > radius * radius) {
+        const float inv = fdiv(1.0f, fsqrt(ox * ox + oy * oy));
+        rx = (ox * inv) * radius; ry = (oy * inv) * radius;
+    } else { rx = ox; ry = oy; }
+    int fail = n;
+#pragma unroll
+    for (int i = 0; i < 4 * NU; ++i) {
+        if (i < n && fail == n) {   // quad-uniform
+            const float4 li = qbc4(R[i >> 2], i);
+            if (det2(li.z, li.w, li.x - rx, li.y - ry) > 0.0f) {
+                float tL, tR;
+                if (!lp1_r<NU>(R, ~0u, i, li, radius, s, tL, tR)) fail = i;
+                else {
+                    const float t = li.z * (ox - li.x) + li.w * (oy - li.y);
+                    if (t < tL) { rx = li.x + tL * li.z; ry = li.y + tL * li.w; }
+                    else if (t > tR) { rx = li.x + tR * li.z; ry = li.y + tR * li.w; }
+                    else { rx = li.x + t * li.z; ry = li.y + t * li.w; }
+                }
+            }
+        }
+    }
+    return fail;
+}
+
+// linearProgram3 from line `begin`; Lb = the same lines in LDS (line i of the outer loop is read from
+// there: its index is dynamic), the projected lines stay in registers (lane s: j = s + 4u)
+template <int NU>
+__device__ __forceinline__ void lp3_r(const float4 (&R)[NU], const float4 *Lb, int n, int begin, float radius, int s,
+                                      float &rx, float &ry)
+{
+    float distance = 0.0f;
+    for (int i = begin; i < n; ++i) {
+        const float4 li = Lb[i];
+        if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
+            float4 P[NU];
+            uint32_t pv = 0;
+#pragma unroll
+            for (int u = 0; u < NU; ++u) {
+                const int j = s + 4 * u;
+                P[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (j < i) {
+                    bool v;
+                    P[u] = proj_line(li, R[u], v);
+                    if (v) pv |= 1u << j;
+                }
+            }
+            pv = (uint32_t)quad_or((int)pv);
+            const float tx = rx, ty = ry;
+            const float ox = -li.w, oy = li.z;   // linearProgram2(projLines, radius, (-d.y, d.x), true)
+            rx = ox * radius; ry = oy * radius;
+            bool fail = false;
+#pragma unroll
+            for (int k = 0; k < 4 * NU; ++k) {
+                if (k < i && !fail && ((pv >> k) & 1u)) {   // quad-uniform
+                    const float4 pk = qbc4(P[k >> 2], k);
+                    if (det2(pk.z, pk.w, pk.x - rx, pk.y - ry) > 0.0f) {
+                        float tL, tR;
+                        if (!lp1_r<NU>(P, pv, k, pk, radius, s, tL, tR)) fail = true;
+                        else if (ox * pk.z + oy * pk.w > 0.0f) { rx = pk.x + tR * pk.z; ry = pk.y + tR * pk.w; }
+                        else { rx = pk.x + tL * pk.z; ry = pk.y + tL * pk.w; }
+                    }
+                }
+            }
+            if (fail) { rx = tx; ry = ty; }
+            distance = det2(li.z, li.w, li.x - rx, li.y - ry);
+        }
+    }
+}
+
 // one ORCA line (Agent::computeNewVelocity, agent branch) of self vs another agent
 __device__ __forceinline__ float4 orca_line(float X0, float Y0, float VX0, float VY0, float R0, float ox, float oy,
                                            float ovx, float ovy, float orr, float invTH, float invTS)
@@ -670,15 +809,16 @@ __device__ __forceinline__ float4 orca_line(float X0, float Y0, float VX0, float
     return make_float4(VX0 + 0.5f * ux, VY0 + 0.5f * uy, dx, dy);
 }
 
-// Agent::computeNeighbors + the agent loop of Agent::computeNewVelocity for a simulator of <= 10 agents
-// (RVO2's KdTree is a single leaf: the neighbours are the in-range slots stably sorted by distSq in slot
-// order), quad-cooperative: lane sq builds the lines of slots sq, sq+4, sq+8 and ranks them itself.
-// `slot(k, x, y, vx, vy, r)` gives observed slot k (agent k + 1) in float32. Lines land in Lb[rank];
-// D is [M] distSq scratch. Returns the number of lines. Shared by cn_step_kernel and cn_debug_orca.
+// Agent::computeNeighbors + the agent loop of Agent::computeNewVelocity for a simulator of <= 13 agents
+// (RVO2's KdTree is a single leaf for <= 10: the neighbours are the in-range slots stably sorted by distSq
+// in slot order), quad-cooperative: lane sq builds the lines of slots sq, sq+4, sq+8 and ranks them itself
+// against the quad's distances, gathered by DPP broadcasts (no LDS round trip).
+// `slot(k, x, y, vx, vy, r)` gives observed slot k (agent k + 1) in float32. Lines land in Lb[rank].
+// Returns the number of lines. Shared by cn_step_kernel and cn_debug_orca.
 template <typename SlotF>
 __device__ __forceinline__ int orca_lines_quad(const SlotF &slot, int M, int sq, float X0, float Y0, float VX0,
                                                float VY0, float R0, float rangeSq, float invTH, float invTS,
-                                               float4 *Lb, float *D)
+                                               float4 *Lb)
 {
     float4 rawv[3];
     float dv[3];
@@ -695,18 +835,20 @@ __device__ __forceinline__ int orca_lines_quad(const SlotF &slot, int M, int sq,
             dv[u] = dx * dx + dy * dy;
             if (dv[u] < rangeSq) inm |= 1u << k;
             rawv[u] = orca_line(X0, Y0, VX0, VY0, R0, x, y, vx, vy, r, invTH, invTS);
-            D[k] = dv[u];
         }
     }
     inm = (uint32_t)quad_or((int)inm);
-    wsync();
+    float dq[12];   // distSq of slot q = 4u + t (lane t's dv[u]), broadcast with the whole quad active
+#pragma unroll
+    for (int q = 0; q < 12; ++q) dq[q] = qbcf(dv[q >> 2], q);
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
         const int k = sq + 4 * u;
         if (k < M && ((inm >> k) & 1u)) {
             int rank = 0;
-            for (int q = 0; q < M; ++q)
-                if (((inm >> q) & 1u) && (D[q] < dv[u] || (D[q] == dv[u] && q < k))) ++rank;
+#pragma unroll
+            for (int q = 0; q < 12; ++q)
+                if (((inm >> q) & 1u) && (dq[q] < dv[u] || (dq[q] == dv[u] && q < k))) ++rank;
             Lb[rank] = rawv[u];
         }
     }
@@ -2187,7 +2329,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                         [&](int k, float &x, float &y, float &vx, float &vy, float &r) {
                             slot_agent(sl, c, eb, elq, EPB, N, iq, k, visq, dmq, rdummy, x, y, vx, vy, r);
                         },
-                        M, sq, X0, Y0, VX0, VY0, R0, rangeSq, invTH, invTS, Lb, sl.nd + h * M);
+                        M, sq, X0, Y0, VX0, VY0, R0, rangeSq, invTH, invTS, Lb);
                 } else {
                     // (1) the quad loads the persisted KdTree order and fills, in that order, the agents'
                     //     positions (XYP[q] = agent perm[q]: self = 0, slot k = k + 1; kept in the projected-
@@ -2424,9 +2566,19 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 if (hq) {
                     const float vmq = sl.vmax[h];
                     float rx, ry;
-                    const int fail_at = lp2_q(Lb, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
-                    STAMP_A(8);
-                    if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
+                    if constexpr (!KD) {   // <= 12 lines: register-resident linear programs
+                        float4 R[3];
+#pragma unroll
+                        for (int u = 0; u < 3; ++u)
+                            R[u] = sq + 4 * u < cnt ? Lb[sq + 4 * u] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        const int fail_at = lp2_r<3>(R, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
+                        STAMP_A(8);
+                        if (fail_at < cnt) lp3_r<3>(R, Lb, cnt, fail_at, vmq, sq, rx, ry);
+                    } else {
+                        const int fail_at = lp2_q(Lb, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
+                        STAMP_A(8);
+                        if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
+                    }
                     STAMP_A(9);
                     if (sq == 0) sl.nv[h] = make_double2((double)rx, (double)ry);
                 }
@@ -3010,8 +3162,7 @@ __global__ void __launch_bounds__(64) cn_orca_kernel(int64_t n, int A, const flo
                                                      const float *__restrict__ self, float nd, float th, float ts,
                                                      float *__restrict__ out)
 {
-    __shared__ float4 Ls[16][9], Ps[16][9];
-    __shared__ float Ds[16][9];
+    __shared__ float4 Ls[16][9];
     const int q = threadIdx.x >> 2, sq = threadIdx.x & 3;
     const int64_t i = (int64_t)blockIdx.x * 16 + q;
     const bool act = i < n;
@@ -3024,13 +3175,16 @@ __global__ void __launch_bounds__(64) cn_orca_kernel(int64_t n, int A, const flo
                 const float *o = a + (k + 1) * 5;
                 x = o[0]; y = o[1]; vx = o[2]; vy = o[3]; r = o[4];
             },
-            M, sq, a[0], a[1], a[2], a[3], a[4], nd * nd, fdiv(1.0f, th), fdiv(1.0f, ts), Ls[q], Ds[q]);
+            M, sq, a[0], a[1], a[2], a[3], a[4], nd * nd, fdiv(1.0f, th), fdiv(1.0f, ts), Ls[q]);
     wsync();
     if (act) {
         const float vmax = self[3 * i], ox = self[3 * i + 1], oy = self[3 * i + 2];
         float rx, ry;
-        const int fail_at = lp2_q(Ls[q], cnt, vmax, ox, oy, sq, rx, ry);
-        if (fail_at < cnt) lp3_q(Ls[q], Ps[q], cnt, fail_at, vmax, sq, rx, ry);
+        float4 R[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) R[u] = sq + 4 * u < cnt ? Ls[q][sq + 4 * u] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const int fail_at = lp2_r<3>(R, cnt, vmax, ox, oy, sq, rx, ry);
+        if (fail_at < cnt) lp3_r<3>(R, Ls[q], cnt, fail_at, vmax, sq, rx, ry);
         if (sq == 0) {
             out[4 * i] = rx; out[4 * i + 1] = ry; out[4 * i + 2] = (float)fail_at; out[4 * i + 3] = (float)cnt;
         }
