@@ -58,18 +58,21 @@ class _EdgeFeatures(torch.autograd.Function):
         x_t = temporal.reshape(E, 2)
         x_s = spatial.reshape(E * N, 2)
         x_r = robot_node.reshape(E, 7)
-        gt = g_t * (t_out > 0)
-        gs = (g_s * (s_out > 0)).reshape(E * N, 64)
+        # weight / bias gradients through the ReLUs: cn_wgrad, one HBM pass each (the ReLU mask applied on
+        # the fly); the node encoder's input h = robot_linear(x_r) is recomputed (E x 3)
+        dWt, dbt = relu_wgrad(g_t, t_out, x_t)
+        dWs, dbs = relu_wgrad(g_s.reshape(E * N, 64), s_out.reshape(E * N, 64), x_s)
+        h = torch.addmm(br, x_r, Wr.t())
+        dWn, dbn = relu_wgrad(g_n, n_out, h)
         gn = g_n * (n_out > 0)
-        h = x_r @ Wr.t() + br
         g_h = gn @ Wn
-        grads = [
-            (g_h @ Wr).reshape(robot_node.shape),
-            (gt @ Wt).reshape(temporal.shape),
-            (gs @ Ws).reshape(spatial.shape),
-            gt.t() @ x_t, gt.sum(0), gs.t() @ x_s, gs.sum(0), g_h.t() @ x_r, g_h.sum(0), gn.t() @ h, gn.sum(0),
-        ]
-        return tuple(grads)
+        dWr, dbr = relu_wgrad(g_h, None, x_r)
+        need = ctx.needs_input_grad
+        # the observations carry no gradient in training; computed only when asked for
+        d_rn = (g_h @ Wr).reshape(robot_node.shape) if need[0] else None
+        d_t = ((g_t * (t_out > 0)) @ Wt).reshape(temporal.shape) if need[1] else None
+        d_s = ((g_s * (s_out > 0)).reshape(E * N, 64) @ Ws).reshape(spatial.shape) if need[2] else None
+        return d_rn, d_t, d_s, dWt, dbt, dWs, dbs, dWr, dbr, dWn, dbn
 
 
 def edge_features(robot_node, temporal, spatial, Wt, bt, Ws, bs, Wr, br, Wn, bn):
@@ -78,6 +81,28 @@ def edge_features(robot_node, temporal, spatial, Wt, bt, Ws, bs, Wr, br, Wn, bn)
         raise EdgeFeaturesUnavailable("the DSRNN edge-feature layers run only as the fused HIP kernel "
                                       "(tensors are on %s)" % robot_node.device)
     return _EdgeFeatures.apply(robot_node, temporal, spatial, Wt, bt, Ws, bs, Wr, br, Wn, bn)
+
+
+def relu_wgrad(dy, relu_out, x):
+    """(dW, db) = ((dy * (relu_out > 0))^T x, column sums of the same) over K rows, on cn_wgrad (one pass;
+    relu_out None: plain dy). dy, relu_out (K, m), x (K, n), min(m, n) <= 8, max(m, n) <= 256."""
+    dy, x = _c(dy), _c(x)
+    K, m = dy.shape
+    n = x.shape[1]
+    mo = _c(relu_out) if relu_out is not None else None
+    L = _lib.lib()
+    dW = torch.empty((m, n), dtype=torch.float32, device=dy.device)
+    db = torch.empty((m,), dtype=torch.float32, device=dy.device)
+    work = torch.empty((max(1, L.cn_wgrad_work_elems(K, m, n)),), dtype=torch.float32, device=dy.device)
+    with torch.cuda.device(dy.device):
+        _lib.check(L.cn_wgrad(_stream(dy.device), K, m, n, dy.data_ptr(), mo.data_ptr() if mo is not None else None,
+                              x.data_ptr(), dW.data_ptr(), db.data_ptr(), work.data_ptr()))
+    return dW, db
+
+
+def skinny(m, n):
+    """The Linear weight gradients cn_wgrad serves (one side tiny)."""
+    return min(m, n) <= 8 and max(m, n) <= 256
 
 
 def wgrad(dy, x, chunk=16384):
@@ -109,8 +134,15 @@ class _Linear(torch.autograd.Function):
         x2, W = ctx.saved_tensors
         dy2 = dy.reshape(-1, W.shape[0]).contiguous()
         dx = (dy2 @ W).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        dW = wgrad(dy2, x2) if ctx.needs_input_grad[1] else None
-        db = dy2.sum(0) if ctx.has_b and ctx.needs_input_grad[2] else None
+        dW = db = None
+        if ctx.needs_input_grad[1] and dy2.is_cuda and skinny(dy2.shape[1], x2.shape[1]):
+            dW, db = relu_wgrad(dy2, None, x2)   # one pass for both
+        elif ctx.needs_input_grad[1]:
+            dW = wgrad(dy2, x2)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = db if db is not None else dy2.sum(0)
+        else:
+            db = None
         return dx, dW, db
 
 

@@ -2,7 +2,7 @@
 import torch
 import torch.nn as nn
 
-from .utils import AddBias, init
+from .utils import AddBias, Linear, init
 
 
 class FixedNormal(torch.distributions.Normal):
@@ -38,7 +38,7 @@ class DiagGaussian(nn.Module):
 
     def __init__(self, num_inputs, num_outputs):
         super().__init__()
-        self.fc_mean = init(nn.Linear(num_inputs, num_outputs), nn.init.orthogonal_, lambda x: nn.init.constant_(x, 0))
+        self.fc_mean = init(Linear(num_inputs, num_outputs), nn.init.orthogonal_, lambda x: nn.init.constant_(x, 0))
         self.logstd = AddBias(torch.zeros(num_outputs))
 
     def forward(self, x):

@@ -28,6 +28,7 @@
  *                   policy_factory[name](config).predict(JointState) (crowd_nav/policy/policy_factory.py:1-17)
  *   cn_lidar_obs     ⟵ CrowdSimDict.generate_ob's 'convgru' observation (crowd_sim_dict.py:96-101) with
  *                   LidarSensor.sensor_spin (crowd_sim/envs/utils/lidarv2.py:398-427) evaluated at reset
+ *   cn_wgrad       ⟵ the weight / bias gradient of the Linear layers with a tiny side (autograd's dy^T x)
  *   cn_attn_pool_fwd / cn_attn_pool_bwd ⟵ EdgeAttention's weighted sum of the spatial edge states
  *                   (srnn_model.py:320-333, torch.bmm(h_spatials^T, attn)) and its gradient
  *
@@ -319,6 +320,16 @@ int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, con
  * dattn[r][n] = sum_h dout[r][h] * hs[r][n][h] (fixed-order reduction). H in {64, 128, 256}. */
 int cn_attn_pool_bwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, const float *dout,
                      float *dhs, float *dattn);
+
+/* Weight gradient of a Linear layer over K rows with a tiny side (ops.linear / the fused input layers'
+ * backward, replacing torch's dy^T x in the reference's autograd of srnn_model.py:160-161,210-211,466 and
+ * distributions.py:74-94): dW[a][j] = sum_k dy'[k][a] x[k][j] and db[a] = sum_k dy'[k][a] with
+ * dy' = dy * (relu_out > 0) when relu_out != NULL (the gradient through a ReLU whose output was relu_out).
+ * dy, relu_out [K][m], x [K][n] contiguous float32; dW [m][n]; db [m] or NULL; min(m, n) <= 8, max(m, n) <= 256.
+ * work: caller-owned device scratch of cn_wgrad_work_elems(K, m, n) floats. Deterministic (fixed order). */
+int64_t cn_wgrad_work_elems(int64_t K, int m, int n);
+int cn_wgrad(void *stream, int64_t K, int m, int n, const float *dy, const float *relu_out, const float *x,
+             float *dW, float *db, float *work);
 
 #ifdef __cplusplus
 }

@@ -193,6 +193,28 @@ def test_masked_gru_kernels_vs_fp64(T, B, F, H):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K,m,n,relu", [(262144, 64, 2, True), (100003, 64, 3, True), (5000, 3, 7, False),
+                                        (70001, 2, 256, False), (1, 1, 256, False), (33, 64, 2, True),
+                                        (1000, 8, 8, True), (4097, 256, 1, False), (2621440, 64, 2, True)])
+def test_wgrad_kernel_vs_fp64(K, m, n, relu):
+    """cn_wgrad (ops.relu_wgrad): dW = (dy * (out > 0))^T x and db = its column sums vs float64. fp32 sums of
+    K products in a fixed order: |error| <= ~K^0.5 eps of the absolute-value sum; tolerance 2e-6 x
+    (|dy'|^T |x|) per entry (the bound a sequential fp32 sum of that length meets with room)."""
+    from crowdnav_dsrnn_amd import ops
+
+    g = torch.Generator().manual_seed(K + m + n)
+    dy = torch.randn(K, m, generator=g)
+    out = torch.randn(K, m, generator=g) if relu else None
+    x = torch.randn(K, n, generator=g)
+    dW, db = ops.relu_wgrad(dy.cuda(), out.cuda() if relu else None, x.cuda())
+    d = dy.double() * (out > 0).double() if relu else dy.double()
+    ref_w, ref_b = d.t() @ x.double(), d.sum(0)
+    bw, bb = d.abs().t() @ x.double().abs(), d.abs().sum(0)
+    np.testing.assert_array_less((dW.cpu().double() - ref_w).abs().numpy(), (2e-6 * bw + 1e-30).numpy())
+    np.testing.assert_array_less((db.cpu().double() - ref_b).abs().numpy(), (2e-6 * bb + 1e-30).numpy())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("R,N,H", [(1, 1, 256), (37, 10, 256), (300, 25, 128), (5, 3, 64)])
 def test_attention_pool_kernels_vs_fp64(R, N, H):
     """cn_attn_pool_fwd / _bwd vs bmm(hs^T, attn) in float64 (srnn_model.py:320-333): output and both
