@@ -69,7 +69,7 @@ struct StepPlan {
     int A;       // agents per RVO2 simulator
     int kd;      // A > 10: RVO2's KdTree order decides ties between equally distant neighbours
     // LDS byte offsets
-    int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_vis, o_nv, o_lines, o_proj, o_nd, o_ns, o_perm,
+    int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_vis, o_nv, o_eg, o_lines, o_proj, o_nd, o_ns, o_perm,
         total;
     int rng_waves;   // phase-5 RNG regions (rng_stride bytes each), laid over o_lines
     int rng_stride;  // CN_PEND_LDS, + CN_GRID_LDS when the plan has room for the spawn's DiscGrid
@@ -108,7 +108,8 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_lane = o;  o = cn_align16(o + H * 8 + H * 4);      // closest distance (f64) + flag word
     p.o_orad = o;  o = cn_align16(o + H * 4);
     p.o_vis = o;   o = cn_align16(o + 3 * H * 4);          // visible mask, dummy mask, frozen max speed
-    p.o_nv = o;    o = cn_align16(o + H * 16);             // new velocity (double2)
+    p.o_nv = o;    o = cn_align16(o + H * 16);             // post-move positions (x [H], y [H])
+    p.o_eg = o;    o = cn_align16(o + H * 4);              // goal-reached / NaN flags
     // ORCA, per human: sorted lines [H][M], projected lines [H][M], neighbour distances; kd: neighbour
     // slots, KdTree agent order
     p.o_lines = o; o = cn_align16(o + ML * H * 16);
@@ -139,7 +140,8 @@ struct SL {
     uint32_t *vis;    // [H] visible-now mask of the human's observed slots (quad path)
     uint32_t *dm;     // [H] dummy-at-creation mask
     float *vmax;      // [H] frozen RVO2 max speed
-    double2 *nv;      // [H] new velocity from the human policy
+    double *npx, *npy; // [H] each: post-move human positions (the phase-5 goal changes read them)
+    uint32_t *eg;     // [H] goal reached (LF_ENDGOAL) / non-finite position (bit 31) after the move
     float4 *lines;    // [M][T]  (kd-tree path)
     float4 *proj;     // [M][T]  linearProgram3's projected lines (kd-tree path)
     float *nd;        // [M][T]
@@ -2057,7 +2059,9 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     sl.vis = (uint32_t *)(smem + P.o_vis);
     sl.dm = sl.vis + P.H;
     sl.vmax = (float *)(sl.vis + 2 * P.H);
-    sl.nv = (double2 *)(smem + P.o_nv);
+    sl.npx = (double *)(smem + P.o_nv);
+    sl.npy = sl.npx + P.H;
+    sl.eg = (uint32_t *)(smem + P.o_eg);
     sl.lines = (float4 *)(smem + P.o_lines);
     sl.proj = (float4 *)(smem + P.o_proj);
     sl.nd = (float *)(smem + P.o_nd);
@@ -2289,6 +2293,135 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     __syncthreads();
     STAMP_A(2);
 
+    // calc_reward ladder + Monitor (crowd_sim.py:907-1094) for env lane re: reads only phase-1 results (pre-move
+    // distances / flags and the robot-only terms), so it runs inside phase 2 on the env lanes (wave 1, after
+    // its own ORCA quads), in the slack while the slowest humans finish their linear programs. The robot's
+    // kinematics update (which the ORCA simulators must not see yet) is applied after phase 2.
+    auto ladder = [&]() {
+        const double rr = RF(sl, R_RAD, re, EPB);
+        const uint32_t flags = sl.rflag[re];
+        const float a0 = sl.act[re], a1 = sl.act[EPB + re];
+        const int eb = re * N;
+        double dmin = INFINITY;
+        bool collision = false, nz_viol = false;
+        int vr_viol = 0, agg = 0;
+        for (int k = 0; k < N; ++k) {
+            const double cd = sl.cd[eb + k];
+            if (cd < 0) { collision = true; break; }
+            else if (cd < dmin) dmin = cd;
+            const uint32_t f = sl.lf[eb + k];
+            vr_viol += (f & LF_VR) ? 1 : 0;
+            agg += (f & LF_NOTREACHED) ? 1 : 0;
+        }
+        // the reference tests the norm zones inside the loop once human 0 is not a collision; the penalty
+        // is read only on the no-collision branch of the ladder, where the loop ran past human 0, so
+        // testing it here (outside the loop: the call's register saves only run when it is taken) is
+        // the same
+        if (c.norm_zones && !collision)
+            nz_viol = robot_norm_zone_violation(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB),
+                                                RF(sl, R_VY, re, EPB), rr, (flags & CN_FLAG_ROBOT_F32) != 0,
+                                                c.norm_zone_lhs);
+        const uint32_t bits = (uint32_t)RF(sl, R_BITS, re, EPB);
+        const bool reaching_goal = (bits & 1u) != 0, inside = (bits & 2u) != 0;
+        if (!reaching_goal) ++agg;
+        const double dist_to_goal = RF(sl, R_D2G, re, EPB);
+        const double gt = RF(sl, R_GT, re, EPB);
+        double reward;
+        int done, event;
+        if (gt >= c.time_limit - 1) { reward = 0; done = 1; event = CN_EV_TIMEOUT; }
+        else if (collision || !inside) { reward = c.collision_penalty; done = 1; event = CN_EV_COLLISION; }
+        else if (reaching_goal) {
+            reward = c.success_reward;
+            if (c.time_factor) reward *= ddiv(c.time_limit - gt, c.time_limit);
+            done = 1; event = CN_EV_REACHGOAL;
+        } else if (dmin < c.discomfort_dist) {
+            reward = (dmin - c.discomfort_dist) * c.discomfort_penalty_factor;
+            done = 0; event = CN_EV_DANGER;
+        } else {
+            reward = c.potential_factor * (-fabs(dist_to_goal) - RF(sl, R_POT, re, EPB));
+            RF(sl, R_POT, re, EPB) = -fabs(dist_to_goal);
+            if (c.norm_zones && nz_viol) reward += c.norm_zone_penalty;
+            done = 0; event = CN_EV_NOTHING;
+        }
+        if (!holo) {
+            const float r_spin = -2.0f * (a1 * a1);
+            const float r_back = a0 < 0 ? -2.0f * fabsf(a0) : 0.0f;
+            if (event == CN_EV_DANGER || event == CN_EV_NOTHING) reward = reward + (double)r_spin + (double)r_back;
+            else reward = (double)(((float)reward + r_spin) + r_back);
+        }
+        if (g.info) {
+            float *info = g.info + orow(ov, ge) * CN_INFO_K;
+            info[CN_INFO_AGG_NAV_TIME] = (float)agg;
+            info[CN_INFO_PATH_VIOLATION] = (float)vr_viol;
+            info[CN_INFO_PERSONAL_VIOLATION] = dmin < c.min_personal_space ? 1.0f : 0.0f;
+            info[CN_INFO_JERK_COST] = (float)RF(sl, R_JERK, re, EPB);
+            info[CN_INFO_DIST_TO_GOAL] = (float)dist_to_goal;
+            info[CN_INFO_SPEED_VIOLATION] = RF(sl, R_SPD, re, EPB) > c.max_walking_speed ? 1.0f : 0.0f;
+            info[CN_INFO_MIN_DIST] = (float)dmin;
+            info[CN_INFO_SCENARIO] = (float)pre_sc;
+            info[CN_INFO_SIDE_LEFT] = (float)RF(sl, R_SL, re, EPB);
+            info[CN_INFO_SIDE_RIGHT] = (float)RF(sl, R_SR, re, EPB);
+            info[CN_INFO_SEPARATION] = (float)RF(sl, R_SEP, re, EPB);
+            info[CN_INFO_OVERFLOW] = (float)pre_ovf;
+        }
+        RF(sl, R_GT, re, EPB) = gt + dt;
+        const double epr = RF(sl, R_EPR, re, EPB) + reward;
+        const int32_t epl = pre_epl + 1;
+        S.ep_return[ge] = epr; S.ep_len[ge] = epl;
+        const int64_t oe = orow(ov, ge);
+        if (g.reward) g.reward[oe] = (float)reward;
+        if (g.done) g.done[oe] = (uint8_t)done;
+        if (g.event) g.event[oe] = (int8_t)event;
+        if (g.ep_return) g.ep_return[oe] = epr;
+        if (g.ep_len) g.ep_len[oe] = epl;
+        sl.rflag[EPB + re] = (uint32_t)done;   // aux word: done
+    };
+    // human kinematics, robot-FOV belief, observation and goal-reached detection of human hh from its new
+    // velocity (agent.py:172-212 step, crowd_sim_dict.py:72-103 generate_ob): called by the lane that
+    // produced the velocity as soon as it has it (ORCA: the quad's lane 0 after its linear programs)
+    auto human_post = [&](int hh, double nvx, double nvy) {
+        const int elh = hh / N, ih = hh - elh * N;
+        const int ghh = (e0 + elh) * N + ih;
+        const double npx = HF(sl, H_PX, hh) + nvx * dt, npy = HF(sl, H_PY, hh) + nvy * dt;
+        S.h_px[ghh] = npx; S.h_py[ghh] = npy; S.h_vx[ghh] = nvx; S.h_vy[ghh] = nvy;
+        // detect_visible(robot, human, robot1=True) on the POST-move state (robot velocity now float32)
+        const double rnx = RF(sl, R_NX, elh, EPB), rny = RF(sl, R_NY, elh, EPB);
+        // the robot's post-move velocity / heading (agent.py:198-212, applied to the state after phase 2):
+        // holonomic = the clipped action, unicycle = the commanded velocity and new heading of phase 1
+        const float rvx = holo ? sl.act[elh] : (float)RF(sl, R_CVX, elh, EPB);
+        const float rvy = holo ? sl.act[EPB + elh] : (float)RF(sl, R_CVY, elh, EPB);
+        const float rth = holo ? 0.0f : (float)RF(sl, R_NTH, elh, EPB);
+        const bool rfin = holo ? (rvx == rvx && rvy == rvy) : isfinite(rth);
+        int rv = c.robot_fov >= 2.0 * CN_PI ? vis360(rfin, rnx, rny, npx, npy) : -1;
+        if (rv < 0) {
+            double fx, fy;
+            if (holo) fov_dir32(atan2f(rvy, rvx), fx, fy);
+            else fov_dir32(rth, fx, fy);
+            rv = in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov, g.cth_r) ? 1 : 0;
+        }
+        double bpx, bpy, bvx, bvy, br;
+        if (rv) {
+            bpx = npx; bpy = npy; bvx = nvx; bvy = nvy; br = HF(sl, H_R, hh);
+        } else {
+            if (rfull) {   // coincident with the robot (or a NaN state): the stored belief, extrapolated
+                bvx = S.b_vx[ghh]; bvy = S.b_vy[ghh]; br = S.b_r[ghh];
+                bpx = S.b_px[ghh] + bvx * dt; bpy = S.b_py[ghh] + bvy * dt;
+            } else {
+                bvx = HF(sl, H_BVX, hh); bvy = HF(sl, H_BVY, hh); br = HF(sl, H_BR, hh);
+                bpx = HF(sl, H_BPX, hh) + bvx * dt; bpy = HF(sl, H_BPY, hh) + bvy * dt;
+            }
+        }
+        S.b_px[ghh] = bpx; S.b_py[ghh] = bpy; S.b_vx[ghh] = bvx; S.b_vy[ghh] = bvy; S.b_r[ghh] = br;
+        const int64_t oh = orow(ov, e0 + elh) * ov.NS + ih;
+        g.spatial[oh * 2] = (float)(bpx - rnx);
+        g.spatial[oh * 2 + 1] = (float)(bpy - rny);
+        uint32_t f = 0u;
+        if (np_norm2(HF(sl, H_GX, hh) - npx, HF(sl, H_GY, hh) - npy) < HF(sl, H_R, hh)) f |= LF_ENDGOAL;
+        if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
+        sl.eg[hh] = f;
+        sl.npx[hh] = npx; sl.npy[hh] = npy;   // post-move positions for the goal changes (HF keeps the pre-move
+                                              // ones: other humans' simulators may still be reading them)
+    };
     // ---- phase 2: human policy (PRE-move state) -------------------------------------------------
     double nvx = 0.0, nvy = 0.0;
     {
@@ -2580,7 +2713,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                         if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
                     }
                     STAMP_A(9);
-                    if (sq == 0) sl.nv[h] = make_double2((double)rx, (double)ry);
+                    if (sq == 0) human_post(h, (double)rx, (double)ry);
                 }
             }
         } else if (hl) {
@@ -2616,143 +2749,24 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             const double n = np_norm2(nx, ny);
             if (n > vpref) { nvx = ddiv(nx, n) * vpref; nvy = ddiv(ny, n) * vpref; }
             else { nvx = nx; nvy = ny; }
-            sl.nv[tid] = make_double2(nvx, nvy);
+            human_post(tid, nvx, nvy);
         }
-        __syncthreads();
-        if (hl) { nvx = sl.nv[tid].x; nvy = sl.nv[tid].y; }
+        if (rl) ladder();
     }
     __syncthreads();
     STAMP_A(3);
 
-    // ---- phase 3: calc_reward ladder + Monitor (env lanes); the robot-only terms came from phase 1 --
+    // ---- robot kinematics, state and observation stores, RNG needs (env lanes) --------------------
     if (rl) {
-        const double rr = RF(sl, R_RAD, re, EPB);
+        // robot kinematics (agent.py:198-212): the post-move state computed in phase 1
         const uint32_t flags = sl.rflag[re];
         const float a0 = sl.act[re], a1 = sl.act[EPB + re];
-        const int eb = re * N;
-        double dmin = INFINITY;
-        bool collision = false, nz_viol = false;
-        int vr_viol = 0, agg = 0;
-        for (int k = 0; k < N; ++k) {
-            const double cd = sl.cd[eb + k];
-            if (cd < 0) { collision = true; break; }
-            else if (cd < dmin) dmin = cd;
-            const uint32_t f = sl.lf[eb + k];
-            vr_viol += (f & LF_VR) ? 1 : 0;
-            agg += (f & LF_NOTREACHED) ? 1 : 0;
-        }
-        // the reference tests the norm zones inside the loop once human 0 is not a collision; the penalty
-        // is read only on the no-collision branch of the ladder, where the loop ran past human 0, so
-        // testing it here (outside the loop: the call's register saves only run when it is taken) is
-        // the same
-        if (c.norm_zones && !collision)
-            nz_viol = robot_norm_zone_violation(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB),
-                                                RF(sl, R_VY, re, EPB), rr, (flags & CN_FLAG_ROBOT_F32) != 0,
-                                                c.norm_zone_lhs);
-        const uint32_t bits = (uint32_t)RF(sl, R_BITS, re, EPB);
-        const bool reaching_goal = (bits & 1u) != 0, inside = (bits & 2u) != 0;
-        if (!reaching_goal) ++agg;
-        const double dist_to_goal = RF(sl, R_D2G, re, EPB);
-        const double gt = RF(sl, R_GT, re, EPB);
-        double reward;
-        int done, event;
-        if (gt >= c.time_limit - 1) { reward = 0; done = 1; event = CN_EV_TIMEOUT; }
-        else if (collision || !inside) { reward = c.collision_penalty; done = 1; event = CN_EV_COLLISION; }
-        else if (reaching_goal) {
-            reward = c.success_reward;
-            if (c.time_factor) reward *= ddiv(c.time_limit - gt, c.time_limit);
-            done = 1; event = CN_EV_REACHGOAL;
-        } else if (dmin < c.discomfort_dist) {
-            reward = (dmin - c.discomfort_dist) * c.discomfort_penalty_factor;
-            done = 0; event = CN_EV_DANGER;
-        } else {
-            reward = c.potential_factor * (-fabs(dist_to_goal) - RF(sl, R_POT, re, EPB));
-            RF(sl, R_POT, re, EPB) = -fabs(dist_to_goal);
-            if (c.norm_zones && nz_viol) reward += c.norm_zone_penalty;
-            done = 0; event = CN_EV_NOTHING;
-        }
-        if (!holo) {
-            const float r_spin = -2.0f * (a1 * a1);
-            const float r_back = a0 < 0 ? -2.0f * fabsf(a0) : 0.0f;
-            if (event == CN_EV_DANGER || event == CN_EV_NOTHING) reward = reward + (double)r_spin + (double)r_back;
-            else reward = (double)(((float)reward + r_spin) + r_back);
-        }
-        if (g.info) {
-            float *info = g.info + orow(ov, ge) * CN_INFO_K;
-            info[CN_INFO_AGG_NAV_TIME] = (float)agg;
-            info[CN_INFO_PATH_VIOLATION] = (float)vr_viol;
-            info[CN_INFO_PERSONAL_VIOLATION] = dmin < c.min_personal_space ? 1.0f : 0.0f;
-            info[CN_INFO_JERK_COST] = (float)RF(sl, R_JERK, re, EPB);
-            info[CN_INFO_DIST_TO_GOAL] = (float)dist_to_goal;
-            info[CN_INFO_SPEED_VIOLATION] = RF(sl, R_SPD, re, EPB) > c.max_walking_speed ? 1.0f : 0.0f;
-            info[CN_INFO_MIN_DIST] = (float)dmin;
-            info[CN_INFO_SCENARIO] = (float)pre_sc;
-            info[CN_INFO_SIDE_LEFT] = (float)RF(sl, R_SL, re, EPB);
-            info[CN_INFO_SIDE_RIGHT] = (float)RF(sl, R_SR, re, EPB);
-            info[CN_INFO_SEPARATION] = (float)RF(sl, R_SEP, re, EPB);
-            info[CN_INFO_OVERFLOW] = (float)pre_ovf;
-        }
-        // robot kinematics (agent.py:198-212): the post-move state computed in phase 1
         if (holo) { RF(sl, R_VX, re, EPB) = a0; RF(sl, R_VY, re, EPB) = a1; }
         else {
             RF(sl, R_TH, re, EPB) = RF(sl, R_NTH, re, EPB);
             RF(sl, R_VX, re, EPB) = RF(sl, R_CVX, re, EPB); RF(sl, R_VY, re, EPB) = RF(sl, R_CVY, re, EPB);
         }
         sl.rflag[re] = flags | CN_FLAG_ROBOT_F32;
-        RF(sl, R_GT, re, EPB) = gt + dt;
-        const double epr = RF(sl, R_EPR, re, EPB) + reward;
-        const int32_t epl = pre_epl + 1;
-        S.ep_return[ge] = epr; S.ep_len[ge] = epl;
-        const int64_t oe = orow(ov, ge);
-        if (g.reward) g.reward[oe] = (float)reward;
-        if (g.done) g.done[oe] = (uint8_t)done;
-        if (g.event) g.event[oe] = (int8_t)event;
-        if (g.ep_return) g.ep_return[oe] = epr;
-        if (g.ep_len) g.ep_len[oe] = epl;
-        sl.rflag[EPB + re] = (uint32_t)done;   // aux word: done
-    }
-    __syncthreads();
-    STAMP_A(4);
-
-    // ---- phase 4: human kinematics, observation, goal-change detection ---------------------------
-    if (hl) {
-        const double npx = HF(sl, H_PX, tid) + nvx * dt, npy = HF(sl, H_PY, tid) + nvy * dt;
-        S.h_px[gh] = npx; S.h_py[gh] = npy; S.h_vx[gh] = nvx; S.h_vy[gh] = nvy;
-        // detect_visible(robot, human, robot1=True) on the POST-move state (robot velocity now float32)
-        const double rnx = RF(sl, R_NX, el, EPB), rny = RF(sl, R_NY, el, EPB);
-        const float rvx = (float)RF(sl, R_VX, el, EPB), rvy = (float)RF(sl, R_VY, el, EPB);
-        const bool rfin = holo ? (rvx == rvx && rvy == rvy) : isfinite((float)RF(sl, R_TH, el, EPB));
-        int rv = c.robot_fov >= 2.0 * CN_PI ? vis360(rfin, rnx, rny, npx, npy) : -1;
-        if (rv < 0) {
-            double fx, fy;
-            if (holo) fov_dir32(atan2f(rvy, rvx), fx, fy);
-            else fov_dir32((float)RF(sl, R_TH, el, EPB), fx, fy);
-            rv = in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov, g.cth_r) ? 1 : 0;
-        }
-        double bpx, bpy, bvx, bvy, br;
-        if (rv) {
-            bpx = npx; bpy = npy; bvx = nvx; bvy = nvy; br = HF(sl, H_R, tid);
-        } else {
-            if (rfull) {   // coincident with the robot (or a NaN state): the stored belief, extrapolated
-                bvx = S.b_vx[gh]; bvy = S.b_vy[gh]; br = S.b_r[gh];
-                bpx = S.b_px[gh] + bvx * dt; bpy = S.b_py[gh] + bvy * dt;
-            } else {
-                bvx = HF(sl, H_BVX, tid); bvy = HF(sl, H_BVY, tid); br = HF(sl, H_BR, tid);
-                bpx = HF(sl, H_BPX, tid) + bvx * dt; bpy = HF(sl, H_BPY, tid) + bvy * dt;
-            }
-        }
-        S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = bvx; S.b_vy[gh] = bvy; S.b_r[gh] = br;
-        const int64_t oh = orow(ov, e0 + el) * ov.NS + i;
-        g.spatial[oh * 2] = (float)(bpx - rnx);
-        g.spatial[oh * 2 + 1] = (float)(bpy - rny);
-        uint32_t f = sl.lf[tid] & ~LF_ENDGOAL;
-        if (np_norm2(HF(sl, H_GX, tid) - npx, HF(sl, H_GY, tid) - npy) < HF(sl, H_R, tid)) f |= LF_ENDGOAL;
-        if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
-        sl.lf[tid] = f;
-        HF(sl, H_PX, tid) = npx; HF(sl, H_PY, tid) = npy;   // post-move positions for the goal changes
-    }
-    __syncthreads();
-    if (rl) {
         const double nx = RF(sl, R_NX, re, EPB), ny = RF(sl, R_NY, re, EPB);
         S.r_px[ge] = nx; S.r_py[ge] = ny;
         S.r_vx[ge] = RF(sl, R_VX, re, EPB); S.r_vy[ge] = RF(sl, R_VY, re, EPB);
@@ -2761,16 +2775,16 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         S.potential[ge] = RF(sl, R_POT, re, EPB);
         const double gt = RF(sl, R_GT, re, EPB);
         S.gtime[ge] = gt;
-        uint32_t flags = sl.rflag[re];
-        if (orca) flags |= CN_FLAG_ORCA_FROZEN;
+        uint32_t flags2 = sl.rflag[re];
+        if (orca) flags2 |= CN_FLAG_ORCA_FROZEN;
         bool endg = false, nan = false;
         for (int k = 0; k < N; ++k) {
-            const uint32_t f = sl.lf[re * N + k];
+            const uint32_t f = sl.eg[re * N + k];
             endg |= (f & LF_ENDGOAL) != 0;
             nan |= (f & 0x80000000u) != 0;
         }
-        if (nan) flags |= CN_FLAG_NAN;
-        S.flags[ge] = flags;
+        if (nan) flags2 |= CN_FLAG_NAN;
+        S.flags[ge] = flags2;
         const int64_t oe = orow(ov, ge);
         float *rn = g.robot_node + oe * 7;
         rn[0] = (float)nx; rn[1] = (float)ny; rn[2] = (float)RF(sl, R_RAD, re, EPB);
@@ -2790,6 +2804,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                               (pre_epl + 1 == 1 ? 8u : 0u);
     }
     __syncthreads();
+    STAMP_A(4);
     STAMP_A(5);
 
     // ---- phase 5: this workgroup's RNG work, one wave per env needing it --------------------------
@@ -2836,7 +2851,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 STAMP_B(e, 5);
             } else {
                 const int b = q * N;
-                en.hpx = &HF(sl, H_PX, b); en.hpy = &HF(sl, H_PY, b); en.hgx = &HF(sl, H_GX, b);
+                en.hpx = sl.npx + b; en.hpy = sl.npy + b; en.hgx = &HF(sl, H_GX, b);
                 en.hgy = &HF(sl, H_GY, b); en.hr = &HF(sl, H_R, b); en.hvp = &HF(sl, H_VP, b); en.hth = &HF(sl, H_TH, b);
                 en.rpx = RF(sl, R_NX, q, EPB); en.rpy = RF(sl, R_NY, q, EPB);
                 en.rgx = RF(sl, R_GX, q, EPB); en.rgy = RF(sl, R_GY, q, EPB); en.rr = RF(sl, R_RAD, q, EPB);

@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_policy.py tests/test_learner.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t1.log 2>&1; rc=$?; tail -3 gpurun_out/t1.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u bench.py --workload c4 > gpurun_out/bench_c4.log 2>&1 || exit $?
-tail -1 gpurun_out/bench_c4.log | cut -c1-200
-timeout -k 10 300 python -u tools/prof_c4_ops.py > gpurun_out/c4_ops.log 2>&1 || exit $?
+true
+bash tools/ab.sh 2
+bash tools/ab.sh 1 --workload c3 --steps 300 --warmup 30
+bash tools/ab.sh 1 --workload c5
