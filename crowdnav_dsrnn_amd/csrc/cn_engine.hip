@@ -44,14 +44,17 @@ __device__ __forceinline__ void wsync()
 // Diagnostic build only (-DCN_STAMPS): per-workgroup s_memtime stamps at phase boundaries, read back
 // with cn_debug_stamps(). The shipped library is built without it (no stamp executes).
 #ifdef CN_STAMPS
-#define CN_NSTAMP 16
+#define CN_NSTAMP 24
 __device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_c[8192 * 4];   // crowded rejection: ensure / cand / test / passes
 __device__ unsigned long long cn_stamp_p[8192 * 2];   // spawn waves: start / end of each env's latest spawn
 #define STAMP_A(k) do { const unsigned sb_ = (unsigned)sb; if (threadIdx.x == 0 && sb_ < 4096) cn_stamp_a[sb_ * CN_NSTAMP + (k)] = clock64(); } while (0)
 #define STAMP_B(w, k) do { if ((threadIdx.x & 63) == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
+// stamp k by thread t (a lane of another wave than thread 0's)
+#define STAMP_T(k, t) do { const unsigned sb_ = (unsigned)sb; if (threadIdx.x == (t) && sb_ < 4096) cn_stamp_a[sb_ * CN_NSTAMP + (k)] = clock64(); } while (0)
 #else
+#define STAMP_T(k, t) do { } while (0)
 #define STAMP_A(k) do { } while (0)
 #define STAMP_B(w, k) do { } while (0)
 #endif
@@ -70,6 +73,7 @@ struct StepPlan {
     int kd;      // A > 10: RVO2's KdTree order decides ties between equally distant neighbours
     // LDS byte offsets
     int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_vis, o_nv, o_eg, o_lines, o_proj, o_nd, o_ns, o_perm,
+        o_hvr,
         total;
     int rng_waves;   // phase-5 RNG regions (rng_stride bytes each), laid over o_lines
     int rng_stride;  // CN_PEND_LDS, + CN_GRID_LDS when the plan has room for the spawn's DiscGrid
@@ -102,7 +106,7 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     int o = 0;
     p.o_renv = o;  o = cn_align16(o + CN_RENV_F * p.EPB * 8);
     p.o_racts = o; o = cn_align16(o + 2 * p.EPB * 4);
-    p.o_rflag = o; o = cn_align16(o + 2 * p.EPB * 4);
+    p.o_rflag = o; o = cn_align16(o + 3 * p.EPB * 4);
     p.o_rvr = o;   o = cn_align16(o + 8 * p.EPB * 8);
     p.o_hum = o;   o = cn_align16(o + CN_HUM_F * H * 8);
     p.o_lane = o;  o = cn_align16(o + H * 8 + H * 4);      // closest distance (f64) + flag word
@@ -117,6 +121,10 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_nd = o;    o = cn_align16(o + ML * H * 4);
     p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * H : 0));
     p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * H : 0));
+    // human velocity rectangles [8][H] (phases 1-2): over the quad path's projected-line / distance scratch,
+    // unused there since the linear programs keep their lines in registers; a region of their own otherwise
+    if (!p.kd && (p.o_ns - p.o_proj) >= 8 * H * 8) p.o_hvr = p.o_proj;
+    else { p.o_hvr = o; o = cn_align16(o + 8 * H * 8); }
     p.rng_waves = 4;
     // the DiscGrid region only where it costs no LDS (the kd-tree path's ORCA scratch is larger than the
     // RNG regions it hosts); the quad path keeps its 3 workgroups per CU
@@ -131,8 +139,9 @@ struct SL {
     int T;            // lane stride of the per-lane arrays
     double *r;        // [CN_RENV_F][EPB]
     float *act;       // [2][EPB] clipped action (holonomic vx,vy / unicycle v,r)
-    uint32_t *rflag;  // [EPB] flags ; [EPB] aux
+    uint32_t *rflag;  // [EPB] flags ; [EPB] aux ; [EPB] humans the reward loop visited (first collision + 1)
     double *rvr;      // [8][EPB] robot VelocityRectangle corners
+    double *hvr;      // [8][H] human VelocityRectangle corners (x0..x3, y0..y3)
     double *h;        // [CN_HUM_F][T]
     double *cd;       // [T]
     uint32_t *lf;     // [T]
@@ -2052,6 +2061,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     sl.act = (float *)(smem + P.o_racts);
     sl.rflag = (uint32_t *)(smem + P.o_rflag);
     sl.rvr = (double *)(smem + P.o_rvr);
+    sl.hvr = (double *)(smem + P.o_hvr);
     sl.h = (double *)(smem + P.o_hum);
     sl.cd = (double *)(smem + P.o_lane);
     sl.lf = (uint32_t *)(smem + P.o_lane + P.H * 8);
@@ -2158,12 +2168,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         }
         sl.act[re] = a0; sl.act[EPB + re] = a1;
         STAMP_A(10);
-        // robot VelocityRectangle (pre-move)
-        double cx[4], cy[4];
-        vel_rect(RF(sl, R_PX, re, EPB), RF(sl, R_PY, re, EPB), RF(sl, R_VX, re, EPB), RF(sl, R_VY, re, EPB),
-                 RF(sl, R_RAD, re, EPB), (sl.rflag[re] & CN_FLAG_ROBOT_F32) != 0, cx, cy);
-        for (int k = 0; k < 4; ++k) { sl.rvr[k * EPB + re] = cx[k]; sl.rvr[(4 + k) * EPB + re] = cy[k]; }
-        STAMP_A(11);
+        STAMP_T(16, 64);
     }
     __syncthreads();
     STAMP_A(1);
@@ -2175,12 +2180,21 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const double vx0 = HF(sl, H_VX, hh), vy0 = HF(sl, H_VY, hh), rad = HF(sl, H_R, hh);
         const double rdx = px - RF(sl, R_PX, elh, EPB), rdy = py - RF(sl, R_PY, elh, EPB);
         sl.cd[hh] = dsqrt(rdx * rdx + rdy * rdy) - rad - RF(sl, R_RAD, elh, EPB);
-        double hcx[4], hcy[4], rcx[4], rcy[4];
+        double hcx[4], hcy[4];
         vel_rect(px, py, vx0, vy0, rad, false, hcx, hcy);
-        for (int k = 0; k < 4; ++k) { rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh]; }
-        uint32_t f = quads_intersect(rcx, rcy, hcx, hcy) ? LF_VR : 0u;
+        for (int k = 0; k < 4; ++k) { sl.hvr[k * 64 + hh] = hcx[k]; sl.hvr[(4 + k) * 64 + hh] = hcy[k]; }
+        // (the path-violation test of this rectangle against the robot's runs in human_post, phase 2: the
+        // robot's rectangle is computed beside this one, on wave 3)
+        uint32_t f = 0u;
         if (!(np_norm2(px - HF(sl, H_GX, hh), py - HF(sl, H_GY, hh)) < rad)) f |= LF_NOTREACHED;
         sl.lf[hh] = f;
+    };
+    // robot VelocityRectangle (pre-move), phase 1 on wave 3
+    auto robot_vr = [&](int q) {
+        double cx[4], cy[4];
+        vel_rect(RF(sl, R_PX, q, EPB), RF(sl, R_PY, q, EPB), RF(sl, R_VX, q, EPB), RF(sl, R_VY, q, EPB),
+                 RF(sl, R_RAD, q, EPB), (sl.rflag[q] & CN_FLAG_ROBOT_F32) != 0, cx, cy);
+        for (int k = 0; k < 4; ++k) { sl.rvr[k * EPB + q] = cx[k]; sl.rvr[(4 + k) * EPB + q] = cy[k]; }
     };
     // robot-only terms of calc_reward (crowd_sim.py:973-1030) and the robot's move (agent.py:172-212);
     // independent of the humans, so the quad path computes them in phase 1 on wave 2
@@ -2239,7 +2253,10 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     // ---- phase 1: visibility of the other agents to human i, frozen simulator parameters --------
     // (quad path: wave 1 computes the per-human reward terms, wave 2 the robot terms meanwhile)
     if (tid >= 64 && tid - 64 < nenv_here * N) reward_terms(tid - 64);
+    STAMP_T(17, 64);
     if (tid >= 128 && tid - 128 < nenv_here) robot_terms(tid - 128);
+    STAMP_T(18, 128);
+    if (tid >= 192 && tid - 192 < nenv_here) robot_vr(tid - 192);
     const bool orca = c.human_policy == CN_POLICY_ORCA;
     uint32_t vis = 0, dm = 0;
     float my_vmax = 0.0f;
@@ -2259,11 +2276,21 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const bool hfin = holo ? (HF(sl, H_VX, tid) == HF(sl, H_VX, tid) && HF(sl, H_VY, tid) == HF(sl, H_VY, tid))
                                : isfinite(HF(sl, H_TH, tid));
         const double px = HF(sl, H_PX, tid), py = HF(sl, H_PY, tid);
-        for (int k = 0; k < N - 1; ++k) {
+        uint32_t undecided = 0;   // 360-degree FOV: decided without the heading except at |v|^2 extremes
+        if (full) {
+#pragma unroll 4
+            for (int k = 0; k < N - 1; ++k) {
+                const int j = eb + (k < i ? k : k + 1);
+                const int v = vis360(hfin, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j));
+                if (v > 0) vis |= 1u << k;
+                if (v < 0) undecided |= 1u << k;
+            }
+        } else undecided = (N - 1 >= 32) ? 0xffffffffu : ((1u << (N - 1)) - 1u);
+        for (uint32_t um = undecided; um; um &= um - 1) {
+            const int k = __ffs(um) - 1;
             const int j = eb + (k < i ? k : k + 1);
-            int v = full ? vis360(hfin, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j)) : -1;
-            if (v < 0) { dir(); v = in_fov(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov, g.cth_h) ? 1 : 0; }
-            if (v) vis |= 1u << k;
+            dir();
+            if (in_fov(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov, g.cth_h)) vis |= 1u << k;
         }
         if (c.robot_visible) {
             int v = full ? vis360(hfin, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB)) : -1;
@@ -2290,6 +2317,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         }
         sl.vis[tid] = vis; sl.dm[tid] = dm; sl.vmax[tid] = my_vmax;
     }
+    STAMP_T(19, 0);
     __syncthreads();
     STAMP_A(2);
 
@@ -2304,15 +2332,15 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const int eb = re * N;
         double dmin = INFINITY;
         bool collision = false, nz_viol = false;
-        int vr_viol = 0, agg = 0;
+        int agg = 0, kv = N;
         for (int k = 0; k < N; ++k) {
             const double cd = sl.cd[eb + k];
-            if (cd < 0) { collision = true; break; }
+            if (cd < 0) { collision = true; kv = k; break; }
             else if (cd < dmin) dmin = cd;
             const uint32_t f = sl.lf[eb + k];
-            vr_viol += (f & LF_VR) ? 1 : 0;
             agg += (f & LF_NOTREACHED) ? 1 : 0;
         }
+        sl.rflag[2 * EPB + re] = (uint32_t)kv;   // the path violations of humans k < kv are counted after phase 2
         // the reference tests the norm zones inside the loop once human 0 is not a collision; the penalty
         // is read only on the no-collision branch of the ladder, where the loop ran past human 0, so
         // testing it here (outside the loop: the call's register saves only run when it is taken) is
@@ -2352,7 +2380,6 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         if (g.info) {
             float *info = g.info + orow(ov, ge) * CN_INFO_K;
             info[CN_INFO_AGG_NAV_TIME] = (float)agg;
-            info[CN_INFO_PATH_VIOLATION] = (float)vr_viol;
             info[CN_INFO_PERSONAL_VIOLATION] = dmin < c.min_personal_space ? 1.0f : 0.0f;
             info[CN_INFO_JERK_COST] = (float)RF(sl, R_JERK, re, EPB);
             info[CN_INFO_DIST_TO_GOAL] = (float)dist_to_goal;
@@ -2416,6 +2443,14 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         g.spatial[oh * 2] = (float)(bpx - rnx);
         g.spatial[oh * 2 + 1] = (float)(bpy - rny);
         uint32_t f = 0u;
+        {   // path violation (crowd_sim.py:951-957): the robot's and the human's pre-move VelocityRectangles
+            double rcx[4], rcy[4], hcx[4], hcy[4];
+            for (int k = 0; k < 4; ++k) {
+                rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh];
+                hcx[k] = sl.hvr[k * 64 + hh]; hcy[k] = sl.hvr[(4 + k) * 64 + hh];
+            }
+            if (quads_intersect(rcx, rcy, hcx, hcy)) f |= LF_VR;
+        }
         if (np_norm2(HF(sl, H_GX, hh) - npx, HF(sl, H_GY, hh) - npy) < HF(sl, H_R, hh)) f |= LF_ENDGOAL;
         if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
         sl.eg[hh] = f;
@@ -2751,7 +2786,9 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             else { nvx = nx; nvy = ny; }
             human_post(tid, nvx, nvy);
         }
+        STAMP_T(21, 64);
         if (rl) ladder();
+        STAMP_T(20, 64);
     }
     __syncthreads();
     STAMP_A(3);
@@ -2778,11 +2815,15 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         uint32_t flags2 = sl.rflag[re];
         if (orca) flags2 |= CN_FLAG_ORCA_FROZEN;
         bool endg = false, nan = false;
+        int vr_viol = 0;
+        const int kv = (int)sl.rflag[2 * EPB + re];
         for (int k = 0; k < N; ++k) {
             const uint32_t f = sl.eg[re * N + k];
             endg |= (f & LF_ENDGOAL) != 0;
             nan |= (f & 0x80000000u) != 0;
+            vr_viol += (k < kv && (f & LF_VR)) ? 1 : 0;
         }
+        if (g.info) g.info[orow(ov, ge) * CN_INFO_K + CN_INFO_PATH_VIOLATION] = (float)vr_viol;
         if (nan) flags2 |= CN_FLAG_NAN;
         S.flags[ge] = flags2;
         const int64_t oe = orow(ov, ge);

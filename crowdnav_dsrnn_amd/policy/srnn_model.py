@@ -178,10 +178,24 @@ class SRNN(nn.Module):
         h_node = rnn_hxs["human_node_rnn"].reshape(B, -1)
         H = h_edge.shape[-1]
 
-        out_t, h_t = self.humanhumanEdgeRNN_temporal(te.reshape(T, B, 64), h_edge[:, 0, :], m)
+        # the temporal and spatial edge RNNs are independent: the temporal one (B rows per step, too few to
+        # fill the GPU) runs on a side stream beside the spatial one (B*N rows); autograd runs each backward
+        # on its forward's stream, so the two overlap there as well
+        side = self._side_stream(te) if T > 1 else None
+        if side is not None:
+            main = torch.cuda.current_stream(te.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                out_t, h_t = self.humanhumanEdgeRNN_temporal(te.reshape(T, B, 64), h_edge[:, 0, :], m)
+        else:
+            out_t, h_t = self.humanhumanEdgeRNN_temporal(te.reshape(T, B, 64), h_edge[:, 0, :], m)
         m_s = m.unsqueeze(-1).expand(T, B, N).reshape(T, B * N)
         out_s, h_s = self.humanhumanEdgeRNN_spatial(se.reshape(T, B * N, 64), h_edge[:, 1:, :].reshape(B * N, H), m_s)
         out_s = out_s.reshape(T, B, N, H)
+        if side is not None:
+            main.wait_stream(side)
+            out_t.record_stream(main)   # allocated on the side stream, consumed here
+            h_t.record_stream(main)
         weighted, _ = self.attn(out_t, out_s)
         outputs, h_n = self.humanNodeRNN(ne.reshape(T, B, 64), out_t, weighted, h_node, m)
 
@@ -192,6 +206,15 @@ class SRNN(nn.Module):
         if infer:
             return self.critic_linear(hidden_critic).squeeze(0), hidden_actor.squeeze(0), rnn_hxs
         return self.critic_linear(hidden_critic).view(-1, 1), hidden_actor.view(-1, self.output_size), rnn_hxs
+
+    def _side_stream(self, t):
+        if not t.is_cuda:
+            return None
+        st = getattr(self, "_side", None)
+        if st is None or st.device != t.device:
+            st = torch.cuda.Stream(device=t.device)
+            self._side = st
+        return st
 
     def _infer_step(self, inputs, rnn_hxs, masks, out_hxs):
         """The act() step without autograd: same arithmetic as the T = 1 path of forward(), but the GRUs

@@ -1,6 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-true
-bash tools/ab.sh 2
-bash tools/ab.sh 1 --workload c3 --steps 300 --warmup 30
-bash tools/ab.sh 1 --workload c5
+bash tools/abn.sh 2 "tools/bin/libcn_base.so tree tools/bin/libcn_d.so"
+bash tools/abn.sh 1 "tools/bin/libcn_base.so tree" --workload c3 --steps 300 --warmup 30

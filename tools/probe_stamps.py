@@ -53,8 +53,8 @@ def run(variant, E=4096, N=10, steps=300):
     eng.reset()
     L = _lib.lib()
     L.cn_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-    a = np.zeros(4096 * 16, np.uint64)
-    b = np.zeros(8192 * 16, np.uint64)
+    a = np.zeros(4096 * 24, np.uint64)
+    b = np.zeros(8192 * 24, np.uint64)
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
     acts = torch.rand((steps, E, 2), generator=g, device="cuda:0") * 0.2 - 0.1
@@ -66,7 +66,7 @@ def run(variant, E=4096, N=10, steps=300):
     L.cn_profile_read(eng._h, ctypes.byref(ta), ctypes.byref(tb), ctypes.byref(n))
     L.cn_debug_stamps(a.ctypes.data_as(ctypes.c_void_p), b.ctypes.data_as(ctypes.c_void_p))
     blocks = (E + (64 // N) - 1) // (64 // N)
-    A = a.reshape(-1, 16)[:blocks].astype(np.int64)
+    A = a.reshape(-1, 24)[:blocks].astype(np.int64)
     d = np.diff(A[:, :7], axis=1)
     print("[%s] kernel A avg %.1f us, kernel B avg %.1f us over %d steps" % (variant, ta.value * 1e3 / n.value,
                                                                           tb.value * 1e3 / n.value, n.value))
@@ -81,7 +81,7 @@ def run(variant, E=4096, N=10, steps=300):
         np.percentile(tot, 95), ", ".join("%s %d" % (nm.split()[0], d[slow, k].mean()) for k, nm in enumerate(names))))
     span = A[:, 6].max() - A[:, 0].min()
     print("  launch span (first start -> last end) %d cycles; start skew max %d" % (span, A[:, 0].max() - A[:, 0].min()))
-    B = b.reshape(-1, 16).astype(np.int64)[:E]
+    B = b.reshape(-1, 24).astype(np.int64)[:E]
     t0 = A[:, 0].min()
     sub = [("p0 human loads", A[:, 12] - A[:, 0]), ("p0 env loads", A[:, 13] - A[:, 12]), ("p0 clip", A[:, 10] - A[:, 13]), ("p0 robot VR", A[:, 11] - A[:, 10]), ("p0 barrier", A[:, 1] - A[:, 11]),
            ("lines+sort", A[:, 7] - A[:, 2]), ("LP2", A[:, 8] - A[:, 7]), ("LP3", A[:, 9] - A[:, 8]), ("VR+terms", A[:, 3] - A[:, 9])]
@@ -94,6 +94,12 @@ def run(variant, E=4096, N=10, steps=300):
         sub = [x for x in sub if not x[0].startswith("p0")]
     for nm, v in sub:
         print("      wave0 %-12s median %8d  max %8d" % (nm, np.median(v), v.max()))
+    if variant != "c3":   # per-wave ends of phases 0-2 (-DCN_STAMPS lanes 0 / 64 / 128), from the phase start
+        per = [("p0 wave1 env load+clip+VR", A[:, 16] - A[:, 0]), ("p1 wave0 visibility", A[:, 19] - A[:, 1]),
+               ("p1 wave1 reward terms", A[:, 17] - A[:, 1]), ("p1 wave2 robot terms", A[:, 18] - A[:, 1]),
+               ("p2 wave1 quads done", A[:, 21] - A[:, 2]), ("p2 wave1 +ladder", A[:, 20] - A[:, 2])]
+        for nm, v in per:
+            print("      %-26s median %8d  max %8d" % (nm, np.median(v), v.max()))
     cur = B[:, 0] >= t0                      # items of the last step only
     res = B[cur & (B[:, 5] >= B[:, 0])]
     goal = B[cur & (B[:, 4] >= B[:, 0]) & (B[:, 5] < B[:, 0])]
