@@ -91,16 +91,22 @@ def lib():
     L.cn_lidar_obs.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_double, ctypes.c_double, vp, vp]
     L.cn_attn_pool_fwd.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int] + [vp] * 3
     L.cn_attn_pool_bwd.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int] + [vp] * 5
-    L.cn_wgrad_work_elems.argtypes = [i64, ctypes.c_int, ctypes.c_int]
-    L.cn_wgrad_work_elems.restype = i64
-    L.cn_wgrad.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int] + [vp] * 6
+    try:
+        L.cn_set_graph_mode.argtypes = [vp, vp, ctypes.c_int]
+        L.cn_wgrad_work_elems.argtypes = [i64, ctypes.c_int, ctypes.c_int]
+        L.cn_wgrad_work_elems.restype = i64
+        L.cn_wgrad.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int] + [vp] * 6
+    except AttributeError:
+        if not os.environ.get("CN_LIB_PATH"):   # an older diagnostic library (A/B runs) may lack them
+            raise
     L.cn_profile.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.cn_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(i64)]
     for f in ("cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
               "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features", "cn_profile",
-              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_wgrad", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict", "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"):
-        getattr(L, f).restype = i32
+              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_wgrad", "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict", "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"):
+        if hasattr(L, f) or not os.environ.get("CN_LIB_PATH"):
+            getattr(L, f).restype = i32
     _lib = L
     return L
 
@@ -116,6 +122,6 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
             "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter",
             "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_wgrad_work_elems", "cn_wgrad",
-            "cn_lidar_obs", "cn_debug_disc_quad",
+            "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad",
             "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict",
             "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"]

@@ -60,6 +60,9 @@ __device__ unsigned long long cn_stamp_p[8192 * 2];   // spawn waves: start / en
 #endif
 #define CN_MAX_A 32
 #define CN_DUMMY_POS 7.0
+#define CN_CTL_NSTEP 12   // work_count words of the device-side step sequence (StepArgs::ctl)
+#define CN_CTL_ALL 13
+#define CN_CTL_DONE 14
 
 // ------------------------------------------------------------------------------------------------
 // launch geometry + LDS plan of kernel A
@@ -1992,6 +1995,14 @@ struct StepArgs {
     float *info;
     double *ep_return;
     int32_t *ep_len;
+    // graph mode (cn_set_graph_mode, the DEVSEQ kernels): the launch's position in the step sequence lives on the device (ctl =
+    // the engine's work_count words: [CN_CTL_NSTEP] launches so far, [CN_CTL_ALL] draw every env's next
+    // spawn, [CN_CTL_DONE] finished workgroups; the last workgroup of a launch advances them), so a launch
+    // has no per-call arguments and a sequence of cn_step calls can be captured in a hipGraph and replayed;
+    // the pointers below are then derived at the top of the kernel. Otherwise the host passes them.
+    uint32_t *ctl;
+    uint32_t *plist_base;   // [3][E + 64] spawn lists
+    uint32_t *rlist_base;   // [3][2E + 64][4] parked-spawn lists
     uint32_t *plist_w;      // envs reset by this launch (their next spawn is drawn by the next launch)
     uint32_t *pcount_w;
     uint32_t *pcount_zero;  // the counter the NEXT launch appends to (triple-buffered), zeroed here
@@ -2038,11 +2049,47 @@ __device__ inline float bbox_dist(float x, float y, float mnx, float mxx, float 
 // template argument so that the MT19937 build carries no Philox registers
 // MIX: a group of a mixed engine (outputs through g.ov); a plain engine's identity view is then a
 // compile-time constant and costs no registers
-template <bool KD, bool PHX, bool MIX>
+// DEVSEQ: graph mode (StepArgs::devseq), a variant of its own so the default launches carry none of it
+template <bool KD, bool PHX, bool MIX, bool DEVSEQ = false>
 __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g, cn_config c)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const OutView ov = MIX ? g.ov : OutView{nullptr, c.human_num};
+    // this launch's spawn / parked-spawn lists (triple-buffered: launch t appends to t % 3, reads (t - 1) % 3,
+    // zeroes (t + 1) % 3) and id, from the device-side step counter
+    const uint32_t ns = DEVSEQ ? g.ctl[CN_CTL_NSTEP] : 0u;
+    if (DEVSEQ) {
+        const int64_t kw = ns % 3u, kr = (ns + 2u) % 3u, kz = (ns + 1u) % 3u;
+        const int64_t ls = (int64_t)g.E + 64, rs = 4 * (2 * (int64_t)g.E + 64);
+        g.plist_w = g.plist_base + kw * ls;
+        g.pcount_w = g.ctl + 2 + kw;
+        g.pcount_zero = g.ctl + 2 + kz;
+        g.rcount_zero = g.ctl + 5 + kz;
+        g.pend.list = g.plist_base + kr * ls;
+        g.pend.count = g.ctl + 2 + kr;
+        g.pend.rlist = g.rlist_base + kr * rs;
+        g.pend.rcount = g.ctl + 5 + kr;
+        g.pend.rlist_w = g.rlist_base + kw * rs;
+        g.pend.rcount_w = g.ctl + 5 + kw;
+        g.pend.launch_id = ((ns + 1u) % 0x7ffffffeu) + 1u;   // nonzero, differs from the neighbours'
+        g.pend.all = g.ctl[CN_CTL_ALL] != 0u;
+    }
+    // the last workgroup to finish advances the sequence (every workgroup has read it by then)
+    // (the atomic carries a register dependency on this workgroup's read of the counter, so the read has
+    // completed before the count can reach the grid size)
+    auto finish = [&]() {
+        if (!DEVSEQ) return;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t dep;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(dep) : "v"(ns));
+            if (atomicAdd(g.ctl + CN_CTL_DONE, 1u + dep) == gridDim.x - 1) {
+                g.ctl[CN_CTL_DONE] = 0u;
+                g.ctl[CN_CTL_ALL] = 0u;
+                g.ctl[CN_CTL_NSTEP] = ns + 1u;
+            }
+        }
+    };
     // the spawn-list counter the NEXT launch appends to (neither read nor appended to by this launch)
     if (blockIdx.x == 0 && threadIdx.x == 0) { *g.pcount_zero = 0u; *g.rcount_zero = 0u; }
     const int sb = (int)blockIdx.x - (g.pend.first ? g.pend.pend_blocks : 0);   // step workgroup index
@@ -2050,6 +2097,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         PendLaunch pl = g.pend;
         pl.ov = ov;
         pend_waves<PHX, KD>(pl, g.s, c, g.E, smem);
+        finish();
         return;
     }
     const int N = c.human_num;
@@ -2908,6 +2956,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     __syncthreads();
     STAMP_A(6);
 #endif
+    finish();
 }
 
 // cn_reset: CrowdSimDict.reset of every env, one wave (single-wave workgroup) per env
@@ -3146,16 +3195,18 @@ struct cn_engine {
                           // [8..11] spawn statistics (PendLaunch::stats)
     uint32_t *plist;      // [3][E] envs whose next spawn kernel A draws
     uint32_t *rlist;      // [3][2E][4] spawns parked by a launch (resumed by the next); counters work_count[5..7]
+    int devseq;           // graph mode (cn_set_graph_mode): the step sequence lives in work_count[12..14]
+    uint32_t ctl_host[4];
+    int pend_all;         // next kernel A draws every env's spawn (after cn_reset / cn_set_state)
+    uint64_t nstep;
     long long spawn_budget;   // clock cycles a spawning wave works per launch before parking (0: never)
     void *pend_mem;       // pending next-episode spawns (PendPtrs)
     PendPtrs pend;
-    int pend_all;         // next kernel A draws every env's spawn (after cn_reset / cn_set_state)
     int pend_blocks;      // spare workgroups of kernel A running spawn waves
     int pend_waves;       // spawning waves per spare workgroup
     int a_lds;            // kernel A dynamic LDS: max(step plan, spawn waves)
     int64_t case_size, counter_offset;
     int rng_grid;
-    uint64_t nstep;
     // kernel timing (cn_profile)
     int prof_on, prof_cap, prof_n;
     hipEvent_t *ev;  // [2]: before the first, after the last launch of the window
@@ -3756,7 +3807,10 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_reset_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
     HIPCHK(hipGetLastError());
-    g->pend_all = 1;   // every env starts a new episode: draw all next spawns in the next kernel A
+    // every env starts a new episode: the next step launch draws all next spawns (host flag; graph mode: the
+    // device flag, stream-ordered)
+    g->pend_all = 1;
+    if (g->devseq) HIPCHK(hipMemsetAsync(g->work_count + CN_CTL_ALL, 1, 4, st));
     return CN_OK;
 }
 
@@ -3765,7 +3819,8 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
 {
     if (!g || !actions || !robot_node || !temporal || !spatial) return set_err(CN_EINVAL, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    // spawn lists, triple-buffered: launch t appends to t%3, reads (t-1)%3, zeroes (t+1)%3
+    // spawn lists, triple-buffered: launch t appends to t%3, reads (t-1)%3, zeroes (t+1)%3 (host sequence;
+    // graph mode keeps it on the device, StepArgs::devseq)
     const int kw = (int)(g->nstep % 3), kr = (int)((g->nstep + 2) % 3), kz = (int)((g->nstep + 1) % 3);
     ++g->nstep;
     const bool prof = g->prof_on && g->prof_n < g->prof_cap;
@@ -3792,6 +3847,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.reward = reward; a.done = done; a.event = event; a.info = info; a.ep_return = ep_return; a.ep_len = ep_len;
     a.E = g->E;
     a.case_size = g->case_size;
+    a.ctl = g->work_count; a.plist_base = g->plist; a.rlist_base = g->rlist;
     a.plist_w = g->plist + (int64_t)kw * (g->E + 64);
     a.pcount_w = g->work_count + 2 + kw;
     a.pcount_zero = g->work_count + 2 + kz;
@@ -3820,10 +3876,34 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
         cn_step_kernel<false, false, false>, cn_step_kernel<false, false, true>, cn_step_kernel<false, true, false>,
         cn_step_kernel<false, true, true>,   cn_step_kernel<true, false, false>,  cn_step_kernel<true, false, true>,
         cn_step_kernel<true, true, false>,   cn_step_kernel<true, true, true>};
+    void (*const kern_dev[4])(StepArgs, cn_config) = {   // graph mode (plain engines)
+        cn_step_kernel<false, false, false, true>, cn_step_kernel<false, true, false, true>,
+        cn_step_kernel<true, false, false, true>, cn_step_kernel<true, true, false, true>};
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
-    hipLaunchKernelGGL(kern[variant], dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
+    if (g->devseq)
+        hipLaunchKernelGGL(kern_dev[variant >> 1], dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
+    else
+        hipLaunchKernelGGL(kern[variant], dim3(grid), dim3(g->plan.T), g->a_lds, st, a, g->c);
     HIPCHK(hipGetLastError());
     if (prof && ++g->prof_n == g->prof_cap) HIPCHK(hipEventRecord(g->ev[1], st));
+    return CN_OK;
+}
+
+int cn_set_graph_mode(cn_engine *g, void *stream, int on)
+{
+    if (!g) return set_err(CN_EINVAL, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    if (g->ngroups || g->rows) return set_err(CN_EUNSUPPORTED, "graph mode: plain engines only (not cn_create_mixed)");
+    if (on && !g->devseq) {   // hand the host sequence to the device
+        g->ctl_host[0] = (uint32_t)g->nstep; g->ctl_host[1] = (uint32_t)g->pend_all; g->ctl_host[2] = 0u;
+        HIPCHK(hipMemcpyAsync(g->work_count + CN_CTL_NSTEP, g->ctl_host, 3 * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));   // ctl_host may be rewritten by the next call
+    } else if (!on && g->devseq) {   // and back
+        HIPCHK(hipMemcpyAsync(g->ctl_host, g->work_count + CN_CTL_NSTEP, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        g->nstep = g->ctl_host[0]; g->pend_all = g->ctl_host[1] ? 1 : 0;
+    }
+    g->devseq = on ? 1 : 0;
     return CN_OK;
 }
 
@@ -3877,7 +3957,9 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
     } else {
         HIPCHK(hipMemcpyAsync(g->state, src, g->state_bytes, hipMemcpyDeviceToDevice, st));
     }
-    g->pend_all = 1;   // pending spawns are keyed by (case_counter, reset_count); redraw them for the new state
+    // pending spawns are keyed by (case_counter, reset_count); redraw them for the new state
+    g->pend_all = 1;
+    if (g->devseq) HIPCHK(hipMemsetAsync(g->work_count + CN_CTL_ALL, 1, 4, st));
     return CN_OK;
 }
 

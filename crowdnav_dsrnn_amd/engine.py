@@ -106,6 +106,12 @@ class CrowdNavEngine:
                 self.ep_len.data_ptr()))
         return self.obs(), self.reward, self.done, self.event, self.info, self.ep_return, self.ep_len
 
+    def set_graph_mode(self, on=True):
+        """cn_set_graph_mode: keep the step sequence on the device so that step() can be captured in a
+        torch.cuda.CUDAGraph (synchronises the current stream)."""
+        with self.torch.cuda.device(self.device):
+            _lib.check(_lib.lib().cn_set_graph_mode(self._h, self._stream(), int(bool(on))))
+
     # -------------------------------------------------------------------------------------------
     def lidar_obs(self, out, lidar, reset_mask=None, enable=True, beams=180, max_range=5.0, robot_radius=0.3):
         """The ConvGRU observation (cn_lidar_obs) into out (E,1,7+beams) f32; lidar (E,beams) f32 holds the

@@ -17,8 +17,15 @@ from .storage import RolloutStorage, SRNNRolloutStorage
 
 
 class RolloutTrainer:
-    def __init__(self, config, envs, actor_critic, agent, deterministic=False):
+    def __init__(self, config, envs, actor_critic, agent, deterministic=False, graphs=None):
+        import os
+
         self.config = config
+        # HIP-graph rollouts (collect); CN_NO_GRAPHS=1 or graphs=False: every rollout eager
+        if graphs is None:
+            graphs = envs.engine.device.type == "cuda" and os.environ.get("CN_NO_GRAPHS", "") in ("", "0")
+        self.graphs = bool(graphs)
+        self._graph, self._warm, self._ep = None, False, None
         self.envs = envs
         self.ac = actor_critic
         self.agent = agent
@@ -48,11 +55,8 @@ class RolloutTrainer:
         self.num_updates = max(int(config.training.num_env_steps) // config.ppo.num_steps // nenv, 1)
         self.update_index = 0
 
-    @torch.no_grad()
-    def collect(self):
+    def _rollout(self, ep_sum, ep_cnt):
         r = self.rollouts
-        ep_sum = torch.zeros((), dtype=torch.float64, device=self.device)
-        ep_cnt = torch.zeros((), dtype=torch.int64, device=self.device)
         for step in range(r.num_steps):
             obs_s = {k: v[step] for k, v in r.obs.items()} if isinstance(r.obs, dict) else r.obs[step]
             hxs_s = r.hidden(step)
@@ -65,8 +69,44 @@ class RolloutTrainer:
             d = done.bool()
             ep_sum += torch.where(d, ep_ret, torch.zeros_like(ep_ret)).sum()
             ep_cnt += d.sum()
+
+    @torch.no_grad()
+    def collect(self):
+        """num_steps env steps of every env. With graphs (CUDA, the default): the first rollout runs eagerly
+        (it also warms up the libraries), the second is captured once as one HIP graph -- act, cn_step (in
+        graph mode: its launch sequence lives on the device, so its launches have no per-call arguments) and the storage
+        writes of all steps -- and every rollout from then on is one replay of it: the same kernels on the
+        same buffers in the same order, without the ~70 host-side launches per step."""
+        r = self.rollouts
+        if self._ep is None:
+            self._ep = (torch.zeros((), dtype=torch.float64, device=self.device),
+                        torch.zeros((), dtype=torch.int64, device=self.device))
+        ep_sum, ep_cnt = self._ep
+        ep_sum.zero_()
+        ep_cnt.zero_()
+        if self.graphs and self._warm:
+            if self._graph is None:
+                g = torch.cuda.CUDAGraph()
+                step0 = r.step
+                try:
+                    self.envs.engine.set_graph_mode(True)   # cn_step launches without per-call arguments
+                    with torch.cuda.graph(g):   # records only; the replay below runs it
+                        self._rollout(ep_sum, ep_cnt)
+                except RuntimeError as e:   # a capture-unsafe call on this path: stay eager
+                    import warnings
+
+                    warnings.warn("rollout HIP-graph capture failed (%s); running eagerly" % e)
+                    self.graphs = False
+                    g = None
+                r.step = step0
+                self._graph = g
+        if self.graphs and self._graph is not None:
+            self._graph.replay()   # (r.step is back at its start value: num_steps inserts wrap it)
+        else:
+            self._rollout(ep_sum, ep_cnt)
+            self._warm = True
         self.env_steps += r.num_steps * self.envs.num_envs
-        return ep_sum, ep_cnt
+        return ep_sum.clone(), ep_cnt.clone()
 
     def update(self):
         t0 = time.perf_counter()

@@ -185,6 +185,14 @@ int cn_step(cn_engine *eng, void *stream, const float *actions,
             double *ep_return, int32_t *ep_len);
 
 /* State blob (layout: include/crowdnav_state.h). */
+/* Graph mode (on = 1): the step sequence (triple-buffered spawn-list indices, launch ids, the draw-all flag
+ * after cn_reset / cn_set_state) moves from the host into device memory, so cn_step launches carry no
+ * per-call arguments and a sequence of cn_step calls (with the caller's other work) can be captured once in
+ * a hipGraph and replayed (learner RolloutTrainer). Costs the launch's last workgroup one atomic; off by
+ * default (separate kernel variants). Plain engines only (CN_EUNSUPPORTED for cn_create_mixed). Switching
+ * synchronises `stream`. No reference equivalent (its env steps are host processes). */
+int cn_set_graph_mode(cn_engine *eng, void *stream, int on);
+
 int cn_state_bytes(const cn_engine *eng, int64_t *bytes);
 int cn_state_layout_offsets(const cn_config *cfg, int64_t *offsets, int64_t *total_bytes);
 int cn_state_field_info(int field, const char **name, int *type_code, int *count_kind);

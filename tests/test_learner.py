@@ -322,3 +322,47 @@ def test_compact_steps_index_types():
     with pytest.raises(IndexError):
         c[np.int64(T + 1)] = 1.0
     assert len(c) == T + 1 and c.shape[0] == 2
+
+
+@pytest.mark.gpu
+def test_rollout_hip_graph_matches_eager():
+    """RolloutTrainer's HIP-graph rollouts (captured at the second update, replayed after) == eager rollouts,
+    bit for bit, over four updates from the same start (deterministic actions; the PPO updates in between
+    change the weights the replays read). 64 envs x 5 humans, ORCA, holonomic, 16 steps; the engine's
+    device-side launch sequence (spawn lists, launch ids, draw-all flag) makes cn_step capturable."""
+    from crowdnav_dsrnn_amd.config import Config, clone_config
+    from crowdnav_dsrnn_amd.envs import CrowdNavVecEnv
+    from crowdnav_dsrnn_amd.learner.loop import RolloutTrainer
+
+    def run(graphs):
+        c = clone_config(Config())
+        c.sim.human_num = 5
+        c.humans.policy = "orca"
+        c.action_space.kinematics = "holonomic"
+        c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+        c.training.num_processes = 64
+        c.ppo.num_steps = 16
+        c.ppo.num_mini_batch = 1
+        c.ppo.epoch = 2
+        torch.manual_seed(5)
+        envs = CrowdNavVecEnv(c, 64, c.env.seed, "cuda:0", nenv=64, phase="train")
+        pol = make_policy(5, E=64, T=16, device="cuda:0")
+        agent = PPO(pol, c.ppo.clip_param, 2, 1, c.ppo.value_loss_coef, c.ppo.entropy_coef, lr=1e-3,
+                    eps=c.training.eps, max_grad_norm=c.training.max_grad_norm)
+        tr = RolloutTrainer(c, envs, pol, agent, deterministic=True, graphs=graphs)
+        out = []
+        for _ in range(4):
+            st = tr.update()
+            r = tr.rollouts
+            out.append((r.actions.cpu().numpy().copy(), r.rewards.cpu().numpy().copy(),
+                        r.value_preds.cpu().numpy().copy(), st["episodes"]))
+        envs.close()
+        return out, tr._graph is not None
+
+    eager, g0 = run(False)
+    graph, g1 = run(True)
+    assert not g0 and g1
+    for u, (a, b) in enumerate(zip(eager, graph)):
+        for x, y in zip(a[:3], b[:3]):
+            np.testing.assert_array_equal(x, y, err_msg="update %d" % u)
+        assert a[3] == b[3]
