@@ -262,7 +262,8 @@ def gru_gemm_roofline(torch, device, B, H, reps=50):
 def run_c4(args, torch, dist, device, rank, world):
     """env-steps/s over PPO updates, counted like train.py:342-352 (rollout of num_steps
     steps of every env with DSRNN act() in the loop, then the PPO update, all inside the timed region).
-    A "step" here is one update = 128 x E env steps per GPU. Defaults: 10 timed updates, 1 warmup."""
+    A "step" here is one update = 128 x E env steps per GPU. Defaults: 10 timed updates, 2 warmup (eager,
+    then the HIP-graph capture of the rollout)."""
     from crowdnav_dsrnn_amd.config import Config, clone_config
     from crowdnav_dsrnn_amd.envs import CrowdNavVecEnv
     from crowdnav_dsrnn_amd.learner import PPO
@@ -271,7 +272,7 @@ def run_c4(args, torch, dist, device, rank, world):
 
     E, N = args.envs, args.humans
     K = args.steps if args.steps != 2000 else 10
-    W = args.warmup if args.warmup != 100 else 1
+    W = args.warmup if args.warmup != 100 else 2   # (the second update captures the rollout graph)
     c = clone_config(Config())
     c.sim.human_num = N
     c.humans.policy = "orca"

@@ -119,6 +119,112 @@ __global__ __launch_bounds__(256) void cn_gru_bwd_kernel(int64_t B, int H, float
     *(float4 *)(dgh + b * 3 * H + 2 * H + j) = dhn;
 }
 
+// The same step with the bias gradients folded in (the reference's autograd sums dgi / dgh over all T*B
+// rows for b_ih / b_hh: two passes over [T][B][3H] each). Workgroup = CN_GB_RW rows x H columns, thread
+// (row slot, 4 columns); besides dgi / dgh it writes the workgroup's column sums of dr | dz | dn | dhn to
+// part [blocks][4H] (row slots summed in order through LDS); cn_gru_bias_reduce adds the partials of all
+// steps in order (deterministic).
+#define CN_GB_RW 16
+__global__ __launch_bounds__(256) void cn_gru_bwd_bias_kernel(int64_t B, int H, float *__restrict__ acc,
+                                                              const float *__restrict__ m_next,
+                                                              const float *__restrict__ dout,
+                                                              const float *__restrict__ save,
+                                                              const float *__restrict__ hm, float *__restrict__ dgi,
+                                                              float *__restrict__ dgh, float *__restrict__ part)
+{
+    __shared__ float4 red[256][4];
+    const int H4 = H >> 2, slots = 256 / H4;   // H in {64, 128, 256}: 16 / 8 / 4 row slots
+    const int rs = (int)threadIdx.x / H4, j = ((int)threadIdx.x - rs * H4) * 4;
+    float4 sr = make_float4(0.f, 0.f, 0.f, 0.f), sz = sr, sn = sr, shn = sr;
+    const int64_t b0 = (int64_t)blockIdx.x * CN_GB_RW;
+    for (int k = rs; k < CN_GB_RW; k += slots) {
+        const int64_t b = b0 + k;
+        if (b >= B) break;
+        const float m = m_next ? m_next[b] : 1.0f;
+        float4 g = *(const float4 *)(acc + b * H + j);
+        g = make_float4(g.x * m, g.y * m, g.z * m, g.w * m);
+        if (dout) {
+            const float4 d = *(const float4 *)(dout + b * H + j);
+            g = make_float4(g.x + d.x, g.y + d.y, g.z + d.z, g.w + d.w);
+        }
+        const float *s = save + b * 4 * H + j;
+        const float4 r = *(const float4 *)(s), z = *(const float4 *)(s + H), n = *(const float4 *)(s + 2 * H),
+                     hn = *(const float4 *)(s + 3 * H);
+        const float4 hp = *(const float4 *)(hm + b * H + j);
+        float4 a, dr, dz, dn, dhn;
+#define CN_GBWD(c)                                              \
+    {                                                           \
+        const float dnc = g.c * (1.0f - z.c) * (1.0f - n.c * n.c); \
+        const float dzc = g.c * (hp.c - n.c) * z.c * (1.0f - z.c); \
+        const float drc = dnc * hn.c * r.c * (1.0f - r.c);      \
+        a.c = g.c * z.c;                                        \
+        dr.c = drc;                                             \
+        dz.c = dzc;                                             \
+        dn.c = dnc;                                             \
+        dhn.c = dnc * r.c;                                      \
+        sr.c += drc; sz.c += dzc; sn.c += dnc; shn.c += dhn.c;  \
+    }
+        CN_GBWD(x) CN_GBWD(y) CN_GBWD(z) CN_GBWD(w)
+#undef CN_GBWD
+        *(float4 *)(acc + b * H + j) = a;
+        *(float4 *)(dgi + b * 3 * H + j) = dr;
+        *(float4 *)(dgi + b * 3 * H + H + j) = dz;
+        *(float4 *)(dgi + b * 3 * H + 2 * H + j) = dn;
+        *(float4 *)(dgh + b * 3 * H + j) = dr;
+        *(float4 *)(dgh + b * 3 * H + H + j) = dz;
+        *(float4 *)(dgh + b * 3 * H + 2 * H + j) = dhn;
+    }
+    red[threadIdx.x][0] = sr; red[threadIdx.x][1] = sz; red[threadIdx.x][2] = sn; red[threadIdx.x][3] = shn;
+    __syncthreads();
+    if (rs != 0) return;
+    for (int q = 1; q < slots; ++q) {
+        const float4 *o = red[q * H4 + threadIdx.x];
+        sr.x += o[0].x; sr.y += o[0].y; sr.z += o[0].z; sr.w += o[0].w;
+        sz.x += o[1].x; sz.y += o[1].y; sz.z += o[1].z; sz.w += o[1].w;
+        sn.x += o[2].x; sn.y += o[2].y; sn.z += o[2].z; sn.w += o[2].w;
+        shn.x += o[3].x; shn.y += o[3].y; shn.z += o[3].z; shn.w += o[3].w;
+    }
+    float *pw = part + (int64_t)blockIdx.x * 4 * H + j;
+    *(float4 *)(pw) = sr;
+    *(float4 *)(pw + H) = sz;
+    *(float4 *)(pw + 2 * H) = sn;
+    *(float4 *)(pw + 3 * H) = shn;
+}
+
+// db_ih = (sum dr, sum dz, sum dn), db_hh = (sum dr, sum dz, sum dhn) over the rows of part [rows][4H]
+// (every step's workgroup partials), in two deterministic passes: CN_GB_RC row chunks x 64-column slices
+// (thread = column, the workgroup's 4 waves stride the chunk's rows, LDS sum in wave order) into
+// work [CN_GB_RC][4H], then the chunks in order.
+#define CN_GB_RC 64
+__global__ __launch_bounds__(256) void cn_gru_bias_part2_kernel(int64_t rows, int H, const float *__restrict__ part,
+                                                                float *__restrict__ work)
+{
+    __shared__ float red[4][64];
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6, rc = blockIdx.y;
+    const int64_t chunk = (rows + CN_GB_RC - 1) / CN_GB_RC, r0 = rc * chunk;
+    const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
+    float s = 0.0f;
+    if (col < 4 * H)
+        for (int64_t r = r0 + w; r < r1; r += 4) s += part[r * 4 * H + col];
+    red[w][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (w != 0 || col >= 4 * H) return;
+    work[(int64_t)rc * 4 * H + col] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void cn_gru_bias_final_kernel(int H, const float *__restrict__ work,
+                                                                float *__restrict__ db_ih, float *__restrict__ db_hh)
+{
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    if (col >= 4 * H) return;
+    float s = 0.0f;
+    for (int rc = 0; rc < CN_GB_RC; ++rc) s += work[rc * 4 * H + col];
+    const int gate = col / H, u = col - gate * H;
+    if (gate < 2) { db_ih[col] = s; db_hh[col] = s; }
+    else if (gate == 2) db_ih[2 * H + u] = s;
+    else db_hh[2 * H + u] = s;
+}
+
 inline unsigned grid_for(int64_t B, int H) { return (unsigned)((B * (H / 4) + 255) / 256); }
 
 // ------------------------------------------------------------------------------------------------
@@ -352,6 +458,36 @@ int cn_gru_fwd_fused(void *stream, int64_t B, int H, const float *gi, const floa
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_gru_fused_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, B, H, (int)rt, ut,
                        gi, hm, w_hh, b_hh, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+int64_t cn_gru_bias_blocks(int64_t B) { return (B + CN_GB_RW - 1) / CN_GB_RW; }
+
+int cn_gru_bwd_step_bias(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
+                         const float *save, const float *hm, float *dgi, float *dgh, float *part)
+{
+    if (B <= 0 || !(H == 64 || H == 128 || H == 256)) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step_bias: H in {64, 128, 256}");
+    if (!acc || !save || !hm || !dgi || !dgh || !part) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step_bias: null operand");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
+    hipLaunchKernelGGL(cn_gru_bwd_bias_kernel, dim3((unsigned)cn_gru_bias_blocks(B)), dim3(256), 0, (hipStream_t)stream,
+                       B, H, acc, m_next, dout, save, hm, dgi, dgh, part);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+int64_t cn_gru_bias_work_elems(int H) { return (int64_t)CN_GB_RC * 4 * H; }
+
+int cn_gru_bias_reduce(void *stream, int64_t rows, int H, const float *part, float *db_ih, float *db_hh,
+                       float *work)
+{
+    if (rows <= 0 || H <= 0 || (H & 3)) return cn_set_error(CN_EINVAL, "cn_gru_bias_reduce: bad shape");
+    if (!part || !db_ih || !db_hh || !work) return cn_set_error(CN_EINVAL, "cn_gru_bias_reduce: null operand");
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(cn_gru_bias_part2_kernel, dim3((unsigned)((4 * H + 63) / 64), CN_GB_RC), dim3(256), 0,
+                       (hipStream_t)stream, rows, H, part, work);
+    hipLaunchKernelGGL(cn_gru_bias_final_kernel, dim3((unsigned)((4 * H + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, H, (const float *)work, db_ih, db_hh);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }

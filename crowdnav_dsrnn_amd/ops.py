@@ -212,17 +212,32 @@ class _MaskedGRU(torch.autograd.Function):
         dout = dout.contiguous() if dout is not None else None
         dgi = torch.empty((T, B, 3 * H), dtype=torch.float32, device=dev)
         dgh = torch.empty((T, B, 3 * H), dtype=torch.float32, device=dev)
+        # bias gradients folded into the step kernel (column sums per 16-row block, reduced once at the end)
+        nblk = L.cn_gru_bias_blocks(B) if H in (64, 128, 256) else 0
+        part = torch.empty((T, nblk, 4 * H), dtype=torch.float32, device=dev) if nblk else None
         with torch.cuda.device(dev):
             for t in reversed(range(T)):
-                _lib.check(L.cn_gru_bwd_step(st, B, H, acc.data_ptr(), None if t + 1 == T else m[t + 1].data_ptr(),
-                                             dout[t].data_ptr() if dout is not None else None, save[t].data_ptr(),
-                                             hm[t].data_ptr(), dgi[t].data_ptr(), dgh[t].data_ptr()))
+                args = (st, B, H, acc.data_ptr(), None if t + 1 == T else m[t + 1].data_ptr(),
+                        dout[t].data_ptr() if dout is not None else None, save[t].data_ptr(),
+                        hm[t].data_ptr(), dgi[t].data_ptr(), dgh[t].data_ptr())
+                if part is not None:
+                    _lib.check(L.cn_gru_bwd_step_bias(*args, part[t].data_ptr()))
+                else:
+                    _lib.check(L.cn_gru_bwd_step(*args))
                 acc.addmm_(dgh[t], w_hh)
+            if part is not None:
+                db_ih = torch.empty((3 * H,), dtype=torch.float32, device=dev)
+                db_hh = torch.empty((3 * H,), dtype=torch.float32, device=dev)
+                work = torch.empty((L.cn_gru_bias_work_elems(H),), dtype=torch.float32, device=dev)
+                _lib.check(L.cn_gru_bias_reduce(st, T * nblk, H, part.data_ptr(), db_ih.data_ptr(), db_hh.data_ptr(),
+                                                work.data_ptr()))
         dh0 = acc * m[0].unsqueeze(-1)
         dgi2 = dgi.reshape(T * B, 3 * H)
         dgh2 = dgh.reshape(T * B, 3 * H)
+        if part is None:
+            db_ih, db_hh = dgi2.sum(0), dgh2.sum(0)
         dx = (dgi2 @ w_ih).reshape(T, B, -1) if ctx.needs_input_grad[0] else None
-        return (dx, dh0, None, wgrad(dgi2, x2), wgrad(dgh2, hm.reshape(T * B, H)), dgi2.sum(0), dgh2.sum(0))
+        return (dx, dh0, None, wgrad(dgi2, x2), wgrad(dgh2, hm.reshape(T * B, H)), db_ih, db_hh)
 
 
 def masked_gru(x, h0, masks, w_ih, w_hh, b_ih, b_hh):

@@ -253,6 +253,17 @@ int cn_gru_fwd_fused(void *stream, int64_t B, int H, const float *gi, const floa
  * acc <- dL/dh_t * z (the caller then adds dgh W_hh to obtain dL/dhm_t). */
 int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
                     const float *save, const float *hm, float *dgi, float *dgh);
+/* cn_gru_bwd_step with the bias gradients folded in: the same dgi_t / dgh_t / acc, plus the column sums of
+ * dr | dz | dn | dhn of every 16-row block to part [cn_gru_bias_blocks(B)][4H] (H in {64, 128, 256}); after
+ * the last step cn_gru_bias_reduce sums the partials of all steps, part [rows][4H], in a fixed order into
+ * db_ih = (dr, dz, dn) and db_hh = (dr, dz, dhn) sums ([3H] each; work: cn_gru_bias_work_elems(H) floats).
+ * Replaces the reference autograd's two extra passes over [T][B][3H] (dgi.sum(0), dgh.sum(0)). */
+int64_t cn_gru_bias_blocks(int64_t B);
+int cn_gru_bwd_step_bias(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
+                         const float *save, const float *hm, float *dgi, float *dgh, float *part);
+int64_t cn_gru_bias_work_elems(int H);
+int cn_gru_bias_reduce(void *stream, int64_t rows, int H, const float *part, float *db_ih, float *db_hh,
+                       float *work);
 
 /* The ConvGRU observation row of every env, obs [E][7 + beams] float32:
  *   [clip(robot (px, py, radius, gx, gy, v_pref, theta) / max_range, 0, 1), scan].
