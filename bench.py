@@ -259,6 +259,22 @@ def gru_gemm_roofline(torch, device, B, H, reps=50):
             "unfused_addmm_plus_gates_us": round(dt_pair * 1e6, 2)}
 
 
+def dsrnn_flop_per_env_step(N, c):
+    """Algorithmic forward FLOP of the DSRNN policy per env-step (srnn_model.py:409-504 with the config's
+    sizes): 2*M*K per output of every Linear / GRU gate GEMM (gi and gh), attention scores and pooling;
+    the elementwise gate / activation arithmetic is not counted. 6.63 MFLOP at N = 10."""
+    S = c.SRNN
+    He, Hn, emb = S.human_human_edge_rnn_size, S.human_node_rnn_size, S.human_human_edge_embedding_size
+    enc = 2 * 2 * emb * (N + 1) + 2 * 7 * 3 + 2 * 3 * S.human_node_embedding_size
+    edge_gru = 2 * emb * 3 * He + 2 * He * 3 * He                  # gi + gh per edge row
+    att = 2 * He * S.attention_size * (N + 1) + 2 * S.attention_size * N + 2 * He * N
+    node_in = 2 * S.human_node_embedding_size
+    node = 2 * (2 * He) * S.human_node_embedding_size + 2 * node_in * 3 * Hn + 2 * Hn * 3 * Hn + 2 * Hn * S.human_node_output_size
+    out = S.human_node_output_size
+    heads = 2 * (2 * out * out) + 2 * (2 * out * out) + 2 * out + 2 * out * 2
+    return enc + (N + 1) * edge_gru + att + node + heads
+
+
 def run_c4(args, torch, dist, device, rank, world):
     """env-steps/s over PPO updates, counted like train.py:342-352 (rollout of num_steps
     steps of every env with DSRNN act() in the loop, then the PPO update, all inside the timed region).
@@ -298,9 +314,12 @@ def run_c4(args, torch, dist, device, rank, world):
             dist.barrier()
         torch.cuda.synchronize(device)
 
+    from crowdnav_dsrnn_amd import ops
+
     for _ in range(W):
         tr.update()
     barrier()
+    ops.FUSED_TIMING = []   # in-loop HIP events around the spatial-edge GRU's fused steps (its stream)
     t0 = time.perf_counter()
     roll = upd = 0.0
     for _ in range(K):
@@ -317,9 +336,30 @@ def run_c4(args, torch, dist, device, rank, world):
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    timing, ops.FUSED_TIMING = ops.FUSED_TIMING, None
     roof = gru_gemm_roofline(torch, device, E // c.ppo.num_mini_batch * N, 256) if rank == 0 else None
+    if rank == 0 and timing:
+        # the roofline of record: the same kernel timed IN the loop (all its launches of the timed updates)
+        n_launch = sum(T for (_, _, T, _, _) in timing)
+        secs = sum(e0.elapsed_time(e1) for (_, _, _, e0, e1) in timing) / 1e3
+        B0, H0 = timing[0][0], timing[0][1]
+        flop = 2.0 * B0 * H0 * 3 * H0
+        iso = roof
+        tf = flop * n_launch / secs / 1e12
+        roof = dict(iso, achieved=round(tf, 3), frac=round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
+                    avg_launch_us=round(secs / n_launch * 1e6, 2), launches_timed=n_launch,
+                    method="HIP events around every training forward's fused-step loop, on its stream, inside "
+                           "the timed updates",
+                    isolated_avg_launch_us=iso["avg_launch_us"])
     if rank == 0:
         steps_per_update = c.ppo.num_steps * E
+        fps = dsrnn_flop_per_env_step(N, c)
+        # rollout forward + PPO epochs x (forward + 2x backward) over every env-step of the update
+        upd_flop = steps_per_update * fps * (1 + 3 * c.ppo.epoch)
+        upd_s = elapsed / K
+        whole = {"flop_per_update": upd_flop, "flop_per_env_step_fwd": fps,
+                 "achieved": round(upd_flop / upd_s / 1e12, 3), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                 "frac": round(upd_flop / upd_s / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}
         line = {
             "metric": METRIC + " [C4 side measurement: incl. DSRNN act + PPO update]",
             "value": round(world * steps_per_update * K / elapsed, 1),
@@ -331,6 +371,7 @@ def run_c4(args, torch, dist, device, rank, world):
                        "rollout_s_per_update": round(roll / K, 4), "ppo_s_per_update": round(upd / K, 4),
                        "parallelism": "dp%d (env-sharded, PPO grads all-reduced)" % world},
             "roofline": roof,
+            "whole_update_roofline": whole,
         }
         print(json.dumps(line), flush=True)
     envs.close()

@@ -151,6 +151,12 @@ def linear(x, W, b=None):
     return _Linear.apply(x, W, b)
 
 
+# Optional in-loop timing of the fused recurrent steps (bench.py's C4 roofline): a list that receives
+# (rows B, steps T, start event, end event) for every training forward with B >= FUSED_TIMING_MIN_ROWS.
+FUSED_TIMING = None
+FUSED_TIMING_MIN_ROWS = 8192
+
+
 class _MaskedGRU(torch.autograd.Function):
     """srnn_model.py:52-104 (RNNBase._forward_gru): h <- h * mask[t] before step t, then one nn.GRU step.
 
@@ -183,6 +189,10 @@ class _MaskedGRU(torch.autograd.Function):
         gh = None if fused else torch.empty((B, 3 * H), dtype=torch.float32, device=dev)
         whh, bhh = _c(w_hh), _c(b_hh)
         nh = hm.shape[0]
+        timing = FUSED_TIMING if (FUSED_TIMING is not None and fused and B >= FUSED_TIMING_MIN_ROWS) else None
+        if timing is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
         with torch.cuda.device(dev):
             for t in range(T):
                 cur = hm[t % nh]
@@ -197,6 +207,9 @@ class _MaskedGRU(torch.autograd.Function):
                     torch.addmm(b_hh, cur, w_hh.t(), out=gh)
                     _lib.check(L.cn_gru_fwd_step(st, B, H, gi[t].data_ptr(), gh.data_ptr(), cur.data_ptr(), mn,
                                                  out[t].data_ptr(), hn, sv))
+        if timing is not None:
+            ev1.record()
+            timing.append((B, H, T, ev0, ev1))
         if need:
             ctx.save_for_backward(x2, m, w_ih, w_hh, hm, save)
         return out, out[-1].clone()
