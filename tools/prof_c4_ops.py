@@ -32,6 +32,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--part", choices=["all", "rollout"], default="all",
+                    help="rollout: profile one eager rollout (collect) only")
     args = ap.parse_args()
     import torch
     from torch.profiler import ProfilerActivity, profile
@@ -57,13 +59,17 @@ def main():
     pol = Policy(envs.observation_space.spaces, envs.action_space, base="srnn", base_kwargs=c).to(device)
     agent = PPO(pol, c.ppo.clip_param, c.ppo.epoch, c.ppo.num_mini_batch, c.ppo.value_loss_coef,
                 c.ppo.entropy_coef, lr=c.training.lr, eps=c.training.eps, max_grad_norm=c.training.max_grad_norm)
-    tr = RolloutTrainer(c, envs, pol, agent)
+    tr = RolloutTrainer(c, envs, pol, agent, graphs=args.part == "all")
     tr.update()
     torch.cuda.synchronize()
     with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
-        st = tr.update()
-        torch.cuda.synchronize()
-    print("profiled update: rollout %.3f s, ppo %.3f s" % (st["rollout_s"], st["update_s"]))
+        if args.part == "rollout":
+            tr.collect()
+            torch.cuda.synchronize()
+        else:
+            st = tr.update()
+            torch.cuda.synchronize()
+            print("profiled update: rollout %.3f s, ppo %.3f s" % (st["rollout_s"], st["update_s"]))
     rows = collections.defaultdict(lambda: [0, 0.0, None])
     total = 0.0
     for ev in prof.events():
