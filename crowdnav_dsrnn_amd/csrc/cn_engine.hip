@@ -1668,12 +1668,25 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
     const int JP = 128 / W;        // tries per batch a fresh page holds
     GP_LAP(t_walk);
     while (rem) {
-        const int h = __ffsll((long long)rem) - 1;
-        rem &= rem - 1;
+        // The remaining eligible humans draw U at consecutive stream positions until one of them changes its
+        // goal, so all of them are tested at once: lane = human index, rank = its place among them; the
+        // first rank with U <= chance (within the page) changes, the draws of the ranks before it are spent.
         if (m.p + 2 > pg.pb + 128) gpage_build(m, pg, trig);
-        const double U = pg.dbl(m.p);
-        m.p += 2;
-        if (!(U <= chance)) continue;
+        const int avail = (pg.pb + 128 - m.p) >> 1;   // draws left in the page (>= 1)
+        const bool mine = ((rem >> lane) & 1ull) != 0;
+        const int rank = __popcll(rem & ((1ull << lane) - 1ull));
+        bool hit = false;
+        if (mine && rank < avail) hit = pg.dbl(m.p + 2 * rank) <= chance;
+        const uint64_t hits = __ballot(hit);
+        if (!hits) {   // none of the first min(avail, |rem|) changes: their draws are spent
+            const int nr = min(avail, __popcll(rem));
+            rem &= ~__ballot(mine && rank < nr);
+            m.p += 2 * nr;
+            continue;
+        }
+        const int h = __ffsll((long long)hits) - 1;
+        m.p += 2 * (__popcll(rem & ((1ull << h) - 1ull)) + 1);
+        rem &= ~((2ull << h) - 1ull);   // h and the humans before it are done
         dbg += 100;
         double r_self = en.hr[h], vpc = en.hvp[h];
         if (KIND == 1) {

@@ -1,4 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u bench.py --workload c4 > gpurun_out/bench_c4.log 2>&1 || exit $?
-tail -1 gpurun_out/bench_c4.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"]); print(d["roofline"]); print(d["whole_update_roofline"])'
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t1.log 2>&1; rc=$?; tail -3 gpurun_out/t1.log; [ $rc -eq 0 ] || exit $rc
+bash tools/abn.sh 2 "tools/bin/libcn_base.so tree" || exit $?
+bash tools/abn.sh 1 "tools/bin/libcn_base.so tree" --workload c3 --steps 300 --warmup 30 || exit $?
+bash tools/abn.sh 1 "tools/bin/libcn_base.so tree" --workload c5 || exit $?
