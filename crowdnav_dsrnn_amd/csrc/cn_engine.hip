@@ -289,6 +289,41 @@ __device__ inline bool quads_intersect(const double *ax, const double *ay, const
     return true;
 }
 
+__device__ __forceinline__ int quad_or(int x);
+// quads_intersect split over the 4 lanes of a quad: lane s tests the 4 axes of edges 2(s & 1), 2(s & 1) + 1 of
+// quad s >> 1 and the quad ORs "separated" (a separating axis exists iff some lane found one: the same
+// boolean as the sequential early-out loop). Lanes of the quad must run it together.
+__device__ __forceinline__ bool quads_intersect_q(const double *ax, const double *ay, const double *bx, const double *by,
+                                                  int s)
+{
+    // the lane's quad and edges by register selects (no lane-dependent indexing)
+    const bool qb = (s >> 1) != 0, hi = (s & 1) != 0;
+    double Qx[4], Qy[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) { Qx[v] = qb ? bx[v] : ax[v]; Qy[v] = qb ? by[v] : ay[v]; }
+    double ex[2], ey[2];
+    ex[0] = hi ? Qx[3] - Qx[2] : Qx[1] - Qx[0]; ey[0] = hi ? Qy[3] - Qy[2] : Qy[1] - Qy[0];   // edge k0
+    ex[1] = hi ? Qx[0] - Qx[3] : Qx[2] - Qx[1]; ey[1] = hi ? Qy[0] - Qy[3] : Qy[2] - Qy[1];   // edge k0 + 1
+    int sep = 0;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+        if (ex[kk] == 0.0 && ey[kk] == 0.0) continue;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const double nx = t ? ex[kk] : -ey[kk], ny = t ? ey[kk] : ex[kk];
+            double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const double pa = ax[v] * nx + ay[v] * ny, pb = bx[v] * nx + by[v] * ny;
+                amin = pa < amin ? pa : amin; amax = pa > amax ? pa : amax;
+                bmin = pb < bmin ? pb : bmin; bmax = pb > bmax ? pb : bmax;
+            }
+            if (amax < bmin || bmax < amin) sep = 1;
+        }
+    }
+    return quad_or(sep) == 0;
+}
+
 __device__ inline bool inside_world(double px, double py, double r, double half)
 {
     const bool right = (px + r >= half) && (px - r <= half);
@@ -2467,7 +2502,27 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     // human kinematics, robot-FOV belief, observation and goal-reached detection of human hh from its new
     // velocity (agent.py:172-212 step, crowd_sim_dict.py:72-103 generate_ob): called by the lane that
     // produced the velocity as soon as it has it (ORCA: the quad's lane 0 after its linear programs)
-    auto human_post = [&](int hh, double nvx, double nvy) {
+    // path violation of human hh (crowd_sim.py:951-957): the robot's and the human's pre-move
+    // VelocityRectangles intersect; quad version (4 lanes of the human's quad together) and a lane version
+    auto path_vr_q = [&](int hh, int s4) -> bool {
+        const int elh = hh / N;
+        double rcx[4], rcy[4], hcx[4], hcy[4];
+        for (int k = 0; k < 4; ++k) {
+            rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh];
+            hcx[k] = sl.hvr[k * 64 + hh]; hcy[k] = sl.hvr[(4 + k) * 64 + hh];
+        }
+        return quads_intersect_q(rcx, rcy, hcx, hcy, s4);
+    };
+    auto path_vr = [&](int hh) -> bool {
+        const int elh = hh / N;
+        double rcx[4], rcy[4], hcx[4], hcy[4];
+        for (int k = 0; k < 4; ++k) {
+            rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh];
+            hcx[k] = sl.hvr[k * 64 + hh]; hcy[k] = sl.hvr[(4 + k) * 64 + hh];
+        }
+        return quads_intersect(rcx, rcy, hcx, hcy);
+    };
+    auto human_post = [&](int hh, double nvx, double nvy, bool vr) {
         const int elh = hh / N, ih = hh - elh * N;
         const int ghh = (e0 + elh) * N + ih;
         const double npx = HF(sl, H_PX, hh) + nvx * dt, npy = HF(sl, H_PY, hh) + nvy * dt;
@@ -2503,15 +2558,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const int64_t oh = orow(ov, e0 + elh) * ov.NS + ih;
         g.spatial[oh * 2] = (float)(bpx - rnx);
         g.spatial[oh * 2 + 1] = (float)(bpy - rny);
-        uint32_t f = 0u;
-        {   // path violation (crowd_sim.py:951-957): the robot's and the human's pre-move VelocityRectangles
-            double rcx[4], rcy[4], hcx[4], hcy[4];
-            for (int k = 0; k < 4; ++k) {
-                rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh];
-                hcx[k] = sl.hvr[k * 64 + hh]; hcy[k] = sl.hvr[(4 + k) * 64 + hh];
-            }
-            if (quads_intersect(rcx, rcy, hcx, hcy)) f |= LF_VR;
-        }
+        uint32_t f = vr ? LF_VR : 0u;
         if (np_norm2(HF(sl, H_GX, hh) - npx, HF(sl, H_GY, hh) - npy) < HF(sl, H_R, hh)) f |= LF_ENDGOAL;
         if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
         sl.eg[hh] = f;
@@ -2809,7 +2856,8 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                         if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
                     }
                     STAMP_A(9);
-                    if (sq == 0) human_post(h, (double)rx, (double)ry);
+                    const bool vr = path_vr_q(h, sq);   // the whole quad
+                    if (sq == 0) human_post(h, (double)rx, (double)ry, vr);
                 }
             }
         } else if (hl) {
@@ -2845,7 +2893,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
             const double n = np_norm2(nx, ny);
             if (n > vpref) { nvx = ddiv(nx, n) * vpref; nvy = ddiv(ny, n) * vpref; }
             else { nvx = nx; nvy = ny; }
-            human_post(tid, nvx, nvy);
+            human_post(tid, nvx, nvy, path_vr(tid));
         }
         STAMP_T(21, 64);
         if (rl) ladder();
