@@ -76,7 +76,7 @@ struct StepPlan {
     int kd;      // A > 10: RVO2's KdTree order decides ties between equally distant neighbours
     // LDS byte offsets
     int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_vis, o_nv, o_eg, o_lines, o_proj, o_nd, o_ns, o_perm,
-        o_hvr,
+        o_hvr, o_hst,
         total;
     int rng_waves;   // phase-5 RNG regions (rng_stride bytes each), laid over o_lines
     int rng_stride;  // CN_PEND_LDS, + CN_GRID_LDS when the plan has room for the spawn's DiscGrid
@@ -126,8 +126,9 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * H : 0));
     // human velocity rectangles [8][H] (phases 1-2): over the quad path's projected-line / distance scratch,
     // unused there since the linear programs keep their lines in registers; a region of their own otherwise
-    if (!p.kd && (p.o_ns - p.o_proj) >= 8 * H * 8) p.o_hvr = p.o_proj;
-    else { p.o_hvr = o; o = cn_align16(o + 8 * H * 8); }
+    // + the human values human_post stages for the contiguous state / observation stores after phase 2 [7][H]
+    if (!p.kd && (p.o_ns - p.o_proj) >= 15 * H * 8) { p.o_hvr = p.o_proj; p.o_hst = p.o_proj + 8 * H * 8; }
+    else { p.o_hvr = o; p.o_hst = o + 8 * H * 8; o = cn_align16(o + 15 * H * 8); }
     p.rng_waves = 4;
     // the DiscGrid region only where it costs no LDS (the kd-tree path's ORCA scratch is larger than the
     // RNG regions it hosts); the quad path keeps its 3 workgroups per CU
@@ -145,6 +146,7 @@ struct SL {
     uint32_t *rflag;  // [EPB] flags ; [EPB] aux ; [EPB] humans the reward loop visited (first collision + 1)
     double *rvr;      // [8][EPB] robot VelocityRectangle corners
     double *hvr;      // [8][H] human VelocityRectangle corners (x0..x3, y0..y3)
+    double *hst;      // [7][H] human_post's results (vx, vy, belief px, py, vx, vy, r), stored after phase 2
     double *h;        // [CN_HUM_F][T]
     double *cd;       // [T]
     uint32_t *lf;     // [T]
@@ -1929,7 +1931,7 @@ struct PendLaunch {
 template <bool PHX, bool GRID>
 __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_ptrs &S, const cn_config &c, int E, char *smem)
 {
-    const int nw = pl.waves, w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    const int nw = pl.waves, w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (w >= nw) return;
     const int N = c.human_num;
     char *base = smem + w * pl.stride;
@@ -2158,6 +2160,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     sl.rflag = (uint32_t *)(smem + P.o_rflag);
     sl.rvr = (double *)(smem + P.o_rvr);
     sl.hvr = (double *)(smem + P.o_hvr);
+    sl.hst = (double *)(smem + P.o_hst);
     sl.h = (double *)(smem + P.o_hum);
     sl.cd = (double *)(smem + P.o_lane);
     sl.lf = (uint32_t *)(smem + P.o_lane + P.H * 8);
@@ -2526,7 +2529,6 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         const int elh = hh / N, ih = hh - elh * N;
         const int ghh = (e0 + elh) * N + ih;
         const double npx = HF(sl, H_PX, hh) + nvx * dt, npy = HF(sl, H_PY, hh) + nvy * dt;
-        S.h_px[ghh] = npx; S.h_py[ghh] = npy; S.h_vx[ghh] = nvx; S.h_vy[ghh] = nvy;
         // detect_visible(robot, human, robot1=True) on the POST-move state (robot velocity now float32)
         const double rnx = RF(sl, R_NX, elh, EPB), rny = RF(sl, R_NY, elh, EPB);
         // the robot's post-move velocity / heading (agent.py:198-212, applied to the state after phase 2):
@@ -2554,10 +2556,12 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 bpx = HF(sl, H_BPX, hh) + bvx * dt; bpy = HF(sl, H_BPY, hh) + bvy * dt;
             }
         }
-        S.b_px[ghh] = bpx; S.b_py[ghh] = bpy; S.b_vx[ghh] = bvx; S.b_vy[ghh] = bvy; S.b_r[ghh] = br;
-        const int64_t oh = orow(ov, e0 + elh) * ov.NS + ih;
-        g.spatial[oh * 2] = (float)(bpx - rnx);
-        g.spatial[oh * 2 + 1] = (float)(bpy - rny);
+        // staged in LDS: the state / observation stores go out after phase 2 from consecutive lanes (one
+        // lane per quad here would split every 128-B line of a field over several waves' partial writes:
+        // +4 MB of HBM writes per C2 launch, measured)
+        sl.hst[0 * 64 + hh] = nvx; sl.hst[1 * 64 + hh] = nvy;
+        sl.hst[2 * 64 + hh] = bpx; sl.hst[3 * 64 + hh] = bpy; sl.hst[4 * 64 + hh] = bvx; sl.hst[5 * 64 + hh] = bvy;
+        sl.hst[6 * 64 + hh] = br;
         uint32_t f = vr ? LF_VR : 0u;
         if (np_norm2(HF(sl, H_GX, hh) - npx, HF(sl, H_GY, hh) - npy) < HF(sl, H_R, hh)) f |= LF_ENDGOAL;
         if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
@@ -2902,7 +2906,18 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     __syncthreads();
     STAMP_A(3);
 
-    // ---- robot kinematics, state and observation stores, RNG needs (env lanes) --------------------
+    // ---- human state / observation stores (human lanes, consecutive) beside the robot kinematics, state
+    //      and observation stores and RNG needs (env lanes) ---------------------------------------------
+    if (hl) {
+        S.h_px[gh] = sl.npx[tid]; S.h_py[gh] = sl.npy[tid];
+        S.h_vx[gh] = sl.hst[0 * 64 + tid]; S.h_vy[gh] = sl.hst[1 * 64 + tid];
+        const double bpx = sl.hst[2 * 64 + tid], bpy = sl.hst[3 * 64 + tid];
+        S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = sl.hst[4 * 64 + tid]; S.b_vy[gh] = sl.hst[5 * 64 + tid];
+        S.b_r[gh] = sl.hst[6 * 64 + tid];
+        const int64_t oh = orow(ov, e0 + el) * ov.NS + i;
+        g.spatial[oh * 2] = (float)(bpx - RF(sl, R_NX, el, EPB));
+        g.spatial[oh * 2 + 1] = (float)(bpy - RF(sl, R_NY, el, EPB));
+    }
     if (rl) {
         // robot kinematics (agent.py:198-212): the post-move state computed in phase 1
         const uint32_t flags = sl.rflag[re];
@@ -2962,7 +2977,9 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     // earlier launch; an env reset by the previous launch (ep_len == 1) may be redrawn by this launch's
     // spawn waves right now, so it (and every env after cn_reset/cn_set_state) draws inline instead.
     {
-        const int nw = P.rng_waves, w = tid / 64, lane = tid & 63;
+        // the wave index is wave-uniform: readfirstlane keeps it (and every LDS pointer derived from it) in
+        // SGPRs -- as a VGPR value the RNG block's preheader spilled it to scratch (HBM writes every launch)
+        const int nw = P.rng_waves, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
         char *wb = smem + P.o_lines + (w < nw ? w : 0) * P.rng_stride;   // over the ORCA scratch, dead after phase 2
         WRng m;
         m.w = (uint32_t *)wb; m.off = 0; m.lane = lane; m.phx = PHX; m.edbg = -1;
