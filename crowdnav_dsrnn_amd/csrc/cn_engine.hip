@@ -49,6 +49,8 @@ __device__ unsigned long long cn_stamp_a[4096 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_c[8192 * 4];   // crowded rejection: ensure / cand / test / passes
 __device__ unsigned long long cn_stamp_p[8192 * 2];   // spawn waves: start / end of each env's latest spawn
+__device__ unsigned long long cn_stamp_r[8192 * 2];   // every workgroup: start / end on the device-wide 100 MHz clock
+#define STAMP_R(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) cn_stamp_r[blockIdx.x * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define STAMP_A(k) do { const unsigned sb_ = (unsigned)sb; if (threadIdx.x == 0 && sb_ < 4096) cn_stamp_a[sb_ * CN_NSTAMP + (k)] = clock64(); } while (0)
 #define STAMP_B(w, k) do { if ((threadIdx.x & 63) == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
 // stamp k by thread t (a lane of another wave than thread 0's)
@@ -57,6 +59,7 @@ __device__ unsigned long long cn_stamp_p[8192 * 2];   // spawn waves: start / en
 #define STAMP_T(k, t) do { } while (0)
 #define STAMP_A(k) do { } while (0)
 #define STAMP_B(w, k) do { } while (0)
+#define STAMP_R(k) do { } while (0)
 #endif
 #define CN_MAX_A 32
 #define CN_DUMMY_POS 7.0
@@ -1466,12 +1469,18 @@ __device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64
         m.key = seed0;
         m.p = 0;
     } else {
-        if (lane == 0) {
-            uint32_t seed = seed0;
-            for (int k = 0; k < CN_MT_N; ++k) {  // mt19937_seed: sequential Knuth chain
-                mtw[k] = seed;
-                seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(k + 1);
+        // mt19937_seed: the sequential Knuth chain, wave-uniform so it runs on the scalar unit (s_mul_i32 /
+        // s_xor / s_lshr: a few cycles per word instead of a quarter-rate v_mul_lo_u32 chain on one lane);
+        // word j*64 + k is dropped into lane k of a VGPR (v_writelane) and each lane stores its word
+        uint32_t seed = __builtin_amdgcn_readfirstlane(seed0);
+        for (int j = 0; j < (CN_MT_N + 63) / 64; ++j) {
+            int mine = 0;
+#pragma unroll
+            for (int k = 0; k < 64; ++k) {
+                asm("v_writelane_b32 %0, %1, %2" : "+v"(mine) : "s"(seed), "n"(k));
+                seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(j * 64 + k + 1);
             }
+            if (j * 64 + lane < CN_MT_N) mtw[j * 64 + lane] = (uint32_t)mine;
         }
         m.p = CN_MT_N;   // numpy: pos = 624 after seeding, the first draw runs mt19937_gen
     }
@@ -2127,7 +2136,12 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     // the last workgroup to finish advances the sequence (every workgroup has read it by then)
     // (the atomic carries a register dependency on this workgroup's read of the counter, so the read has
     // completed before the count can reach the grid size)
+    STAMP_R(0);
     auto finish = [&]() {
+#ifdef CN_STAMPS
+        __syncthreads();
+        STAMP_R(1);
+#endif
         if (!DEVSEQ) return;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -4047,6 +4061,14 @@ int cn_debug_stamps_c(unsigned long long *c, unsigned long long *p)
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpyFromSymbol(c, HIP_SYMBOL(cn_stamp_c), sizeof(unsigned long long) * 8192 * 4));
     HIPCHK(hipMemcpyFromSymbol(p, HIP_SYMBOL(cn_stamp_p), sizeof(unsigned long long) * 8192 * 2));
+    return CN_OK;
+}
+
+// per-workgroup start / end on the device-wide 100 MHz realtime clock
+int cn_debug_stamps_r(unsigned long long *r)
+{
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(r, HIP_SYMBOL(cn_stamp_r), sizeof(unsigned long long) * 8192 * 2));
     return CN_OK;
 }
 

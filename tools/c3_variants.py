@@ -1,6 +1,6 @@
-"""Diagnostic: C3 step time with parts of the RNG work switched off, to size the rejection-loop tail.
+"""Diagnostic: C3 (or C2) step time with parts of the RNG work switched off, to size the goal-change work.
 
-    python tools/c3_variants.py [steps]
+    python tools/c3_variants.py [steps] [c3|c2]
 
 Variants: the C3 workload as benched; without end-goal changing; without random goal changing; without
 either. Each: 30 warmup steps, then `steps` timed launches (HIP events on the engine's stream).
@@ -15,13 +15,18 @@ from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config  # no
 from crowdnav_dsrnn_amd.engine import CrowdNavEngine  # noqa: E402
 
 
-def run(end_goal, rand_goal, steps, E=4096, N=25):
+def run(end_goal, rand_goal, steps, E=4096, wl="c3"):
     c = clone_config(Config())
-    c.sim.human_num = N
     c.humans.policy = "orca"
-    c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
-    c.action_space.kinematics = "holonomic"
-    c.robot.FOV = c.humans.FOV = 1.0
+    if wl == "c3":
+        c.sim.human_num = 25
+        c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
+        c.action_space.kinematics = "holonomic"
+        c.robot.FOV = c.humans.FOV = 1.0
+    else:   # bench.py's C2 workload
+        c.sim.human_num = 10
+        c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+        c.action_space.kinematics = "unicycle"
     c.humans.end_goal_changing = end_goal
     c.humans.random_goal_changing = rand_goal
     eng = CrowdNavEngine(make_cn_config(c, num_envs=E, phase="train"), "cuda:0")
@@ -46,5 +51,6 @@ def run(end_goal, rand_goal, steps, E=4096, N=25):
 
 if __name__ == "__main__":
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    wl = sys.argv[2] if len(sys.argv) > 2 else "c3"
     for eg, rg in ((True, True), (False, True), (True, False), (False, False)):
-        run(eg, rg, steps)
+        run(eg, rg, steps, wl=wl)

@@ -81,6 +81,33 @@ def run(variant, E=4096, N=10, steps=300):
         np.percentile(tot, 95), ", ".join("%s %d" % (nm.split()[0], d[slow, k].mean()) for k, nm in enumerate(names))))
     span = A[:, 6].max() - A[:, 0].min()
     print("  launch span (first start -> last end) %d cycles; start skew max %d" % (span, A[:, 0].max() - A[:, 0].min()))
+    # the whole grid on the device-wide 100 MHz clock (s_memtime above is per XCD: durations only)
+    L.cn_debug_stamps_r.argtypes = [ctypes.c_void_p]
+    r = np.zeros(8192 * 2, np.uint64)
+    L.cn_debug_stamps_r(r.ctypes.data_as(ctypes.c_void_p))
+    R = r.reshape(-1, 2).astype(np.int64)
+    live = np.nonzero(R[:, 1] > 0)[0]
+    if len(live):
+        R = R[:live.max() + 1]
+        t0r = R[R[:, 0] > 0, 0].min()
+        st, en = (R[:, 0] - t0r) * 10, (R[:, 1] - t0r) * 10     # ns
+        kd = variant == "c3"
+        nb = len(R)
+        is_step = np.zeros(nb, bool)
+        if kd:
+            is_step[nb - blocks:] = True
+        else:
+            is_step[:blocks] = True
+        print("  grid timeline (ns from the first workgroup's start; %d step + %d spawn workgroups):" % (
+            is_step.sum(), (~is_step).sum()))
+        for nm, sel in (("step", is_step), ("spawn", ~is_step)):
+            if sel.any():
+                print("    %-5s start median %6d max %6d | end median %6d p95 %6d max %6d | duration median %6d max %6d" % (
+                    nm, np.median(st[sel]), st[sel].max(), np.median(en[sel]), np.percentile(en[sel], 95), en[sel].max(),
+                    np.median(en[sel] - st[sel]), (en[sel] - st[sel]).max()))
+        last = np.argsort(-en)[:8]
+        print("    last to end: " + ", ".join("%s#%d [%d, %d]" % ("step" if is_step[k] else "spawn", k, st[k], en[k])
+                                              for k in last))
     B = b.reshape(-1, 24).astype(np.int64)[:E]
     t0 = A[:, 0].min()
     sub = [("p0 human loads", A[:, 12] - A[:, 0]), ("p0 env loads", A[:, 13] - A[:, 12]), ("p0 clip", A[:, 10] - A[:, 13]), ("p0 robot VR", A[:, 11] - A[:, 10]), ("p0 barrier", A[:, 1] - A[:, 11]),
