@@ -50,6 +50,8 @@ __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_c[8192 * 4];   // crowded rejection: ensure / cand / test / passes
 __device__ unsigned long long cn_stamp_p[8192 * 2];   // spawn waves: start / end of each env's latest spawn
 __device__ unsigned long long cn_stamp_r[8192 * 2];   // every workgroup: start / end on the device-wide 100 MHz clock
+__device__ unsigned long long cn_stamp_s[8192 * 16];   // spawn_env: start, seeded, robot, after human i (3 + i)
+#define STAMP_S(e, k) do { if (lane == 0 && (e) >= 0 && (e) < 8192) cn_stamp_s[(e) * 16 + (k)] = clock64(); } while (0)
 #define STAMP_R(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) cn_stamp_r[blockIdx.x * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define STAMP_A(k) do { const unsigned sb_ = (unsigned)sb; if (threadIdx.x == 0 && sb_ < 4096) cn_stamp_a[sb_ * CN_NSTAMP + (k)] = clock64(); } while (0)
 #define STAMP_B(w, k) do { if ((threadIdx.x & 63) == 0 && (w) < 8192) cn_stamp_b[(w) * CN_NSTAMP + (k)] = clock64(); } while (0)
@@ -60,6 +62,7 @@ __device__ unsigned long long cn_stamp_r[8192 * 2];   // every workgroup: start 
 #define STAMP_A(k) do { } while (0)
 #define STAMP_B(w, k) do { } while (0)
 #define STAMP_R(k) do { } while (0)
+#define STAMP_S(e, k) do { } while (0)
 #endif
 #define CN_MAX_A 32
 #define CN_DUMMY_POS 7.0
@@ -1458,6 +1461,7 @@ __device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64
     const int N = c.human_num;
     const double R = c.circle_radius;
     const int W0 = i0;
+    STAMP_S(gidx, 0);
     if (i0 == 0) {
     uint32_t *mtw = m.w;
     m.off = 0;   // a fresh stream: the key at the start of the ring
@@ -1485,6 +1489,7 @@ __device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64
         m.p = CN_MT_N;   // numpy: pos = 624 after seeding, the first draw runs mt19937_gen
     }
     wsync();
+    STAMP_S(gidx, 1);
     m.have1 = false; m.slid = false;
     ovf = 0;
     en.rr = c.robot_radius;
@@ -1511,6 +1516,7 @@ __device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64
         rth = CN_PI / 2;
     }
     }   // i0 == 0
+    STAMP_S(gidx, 2);
     const int W = cand_words(sc);
     for (int i = i0; i < N; ++i) {
         if (deadline && i > W0 && (long long)clock64() > deadline) return i;   // park (wave-uniform clock)
@@ -1536,6 +1542,7 @@ __device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64
             en.hth[i] = m.sl[256 + tw]; en.hvp[i] = m.sl[320 + tw]; en.hr[i] = rad;
         }
         wsync();
+        if (i < 13) STAMP_S(gidx, 3 + i);
     }
     return N;
 }
@@ -4064,11 +4071,12 @@ int cn_debug_stamps_c(unsigned long long *c, unsigned long long *p)
     return CN_OK;
 }
 
-// per-workgroup start / end on the device-wide 100 MHz realtime clock
-int cn_debug_stamps_r(unsigned long long *r)
+// per-workgroup start / end on the device-wide 100 MHz realtime clock; spawn_env's segment stamps
+int cn_debug_stamps_r(unsigned long long *r, unsigned long long *sp)
 {
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpyFromSymbol(r, HIP_SYMBOL(cn_stamp_r), sizeof(unsigned long long) * 8192 * 2));
+    if (sp) HIPCHK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(cn_stamp_s), sizeof(unsigned long long) * 8192 * 16));
     return CN_OK;
 }
 

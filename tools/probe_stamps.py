@@ -82,9 +82,9 @@ def run(variant, E=4096, N=10, steps=300):
     span = A[:, 6].max() - A[:, 0].min()
     print("  launch span (first start -> last end) %d cycles; start skew max %d" % (span, A[:, 0].max() - A[:, 0].min()))
     # the whole grid on the device-wide 100 MHz clock (s_memtime above is per XCD: durations only)
-    L.cn_debug_stamps_r.argtypes = [ctypes.c_void_p]
+    L.cn_debug_stamps_r.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     r = np.zeros(8192 * 2, np.uint64)
-    L.cn_debug_stamps_r(r.ctypes.data_as(ctypes.c_void_p))
+    L.cn_debug_stamps_r(r.ctypes.data_as(ctypes.c_void_p), None)
     R = r.reshape(-1, 2).astype(np.int64)
     live = np.nonzero(R[:, 1] > 0)[0]
     if len(live):

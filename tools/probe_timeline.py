@@ -37,7 +37,8 @@ def main(steps=400, wl="c2", E=4096):
     eng = CrowdNavEngine(make_cn_config(c, num_envs=E), "cuda:0")
     eng.reset()
     L = _lib.lib()
-    L.cn_debug_stamps_r.argtypes = [ctypes.c_void_p]
+    L.cn_debug_stamps_r.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    sp = np.zeros(8192 * 16, np.uint64)
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
     if wl == "c2":
@@ -55,7 +56,7 @@ def main(steps=400, wl="c2", E=4096):
         _lib.check(L.cn_profile(eng._h, 1, 1))
         eng.step(acts[s])
         _lib.check(L.cn_profile_read(eng._h, ctypes.byref(ta), ctypes.byref(tb), ctypes.byref(n)))
-        L.cn_debug_stamps_r(r.ctypes.data_as(ctypes.c_void_p))
+        L.cn_debug_stamps_r(r.ctypes.data_as(ctypes.c_void_p), sp.ctypes.data_as(ctypes.c_void_p))
         R = r.reshape(-1, 2).astype(np.int64)
         live = np.nonzero(R[:, 1] > 0)[0]
         R = R[:live.max() + 1]
@@ -71,6 +72,18 @@ def main(steps=400, wl="c2", E=4096):
                      np.percentile(en[step_sel], 50), prev_done))
         prev_done = d
     _lib.check(L.cn_profile(eng._h, 0, 0))
+    # spawn_env segments (the latest spawn of each env: seeding, robot, humans 0..N-1), cycles
+    Sg = sp.reshape(-1, 16).astype(np.int64)[:E]
+    ok = Sg[:, 3 + N - 1] > Sg[:, 0]
+    if ok.any():
+        Sg = Sg[ok]
+        seg = np.diff(Sg[:, :3 + N], axis=1)
+        print("[%s] spawn_env segments over %d envs' latest spawn (cycles, median / p90): seed %d / %d, robot %d / %d, "
+              "humans %s; total %d / %d" % (
+                  wl, ok.sum(), np.median(seg[:, 0]), np.percentile(seg[:, 0], 90), np.median(seg[:, 1]),
+                  np.percentile(seg[:, 1], 90),
+                  " ".join("%d" % v for v in np.median(seg[:, 2:], 0)), np.median(Sg[:, 2 + N] - Sg[:, 0]),
+                  np.percentile(Sg[:, 2 + N] - Sg[:, 0], 90)))
     a = np.asarray(rows)
     print("[%s] launch | kernel us | last step-WG end us | last spawn-WG end us | median step-WG end | "
           "resets drawn ahead (prev done)" % wl)
