@@ -50,6 +50,7 @@ __device__ unsigned long long cn_stamp_b[8192 * CN_NSTAMP];
 __device__ unsigned long long cn_stamp_c[8192 * 4];   // crowded rejection: ensure / cand / test / passes
 __device__ unsigned long long cn_stamp_p[8192 * 2];   // spawn waves: start / end of each env's latest spawn
 __device__ unsigned long long cn_stamp_r[8192 * 2];   // every workgroup: start / end on the device-wide 100 MHz clock
+__device__ unsigned long long cn_lp3_cnt[2 + 12];   // lp3 sub-problems solved / visited by the replay (all launches)
 __device__ unsigned long long cn_stamp_s[8192 * 16];   // spawn_env: start, seeded, robot, after human i (3 + i)
 #define STAMP_S(e, k) do { if (lane == 0 && (e) >= 0 && (e) < 8192) cn_stamp_s[(e) * 16 + (k)] = clock64(); } while (0)
 #define STAMP_R(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) cn_stamp_r[blockIdx.x * 2 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -65,6 +66,9 @@ __device__ unsigned long long cn_stamp_s[8192 * 16];   // spawn_env: start, seed
 #define STAMP_S(e, k) do { } while (0)
 #endif
 #define CN_MAX_A 32
+#ifndef CN_LP3_W
+#define CN_LP3_W 12   // linearProgram3 sub-problems solved ahead per infeasible human (lp3_tasks); the rest inline
+#endif
 #define CN_DUMMY_POS 7.0
 #define CN_CTL_NSTEP 12   // work_count words of the device-side step sequence (StepArgs::ctl)
 #define CN_CTL_ALL 13
@@ -82,7 +86,7 @@ struct StepPlan {
     int kd;      // A > 10: RVO2's KdTree order decides ties between equally distant neighbours
     // LDS byte offsets
     int o_renv, o_racts, o_rflag, o_rvr, o_hum, o_lane, o_orad, o_vis, o_nv, o_eg, o_lines, o_proj, o_nd, o_ns, o_perm,
-        o_hvr, o_hst,
+        o_hvr, o_hst, o_l3b, o_l3r, o_l3k,
         total;
     int rng_waves;   // phase-5 RNG regions (rng_stride bytes each), laid over o_lines
     int rng_stride;  // CN_PEND_LDS, + CN_GRID_LDS when the plan has room for the spawn's DiscGrid
@@ -135,6 +139,11 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     // + the human values human_post stages for the contiguous state / observation stores after phase 2 [7][H]
     if (!p.kd && (p.o_ns - p.o_proj) >= 15 * H * 8) { p.o_hvr = p.o_proj; p.o_hst = p.o_proj + 8 * H * 8; }
     else { p.o_hvr = o; p.o_hst = o + 8 * H * 8; o = cn_align16(o + 15 * H * 8); }
+    // quad path: the workgroup's linearProgram3 sub-problems (lp3_tasks): per human fail | n << 8, results
+    // [H][12] (phase 2 only: under the RNG regions)
+    p.o_l3b = o;   o = cn_align16(o + (p.kd ? 0 : H * 4));
+    p.o_l3r = o;   o = cn_align16(o + (p.kd ? 0 : H * 12 * 8));
+    p.o_l3k = o;   o = cn_align16(o + (p.kd ? 0 : H * 12));
     p.rng_waves = 4;
     // the DiscGrid region only where it costs no LDS (the kd-tree path's ORCA scratch is larger than the
     // RNG regions it hosts); the quad path keeps its 3 workgroups per CU
@@ -775,6 +784,44 @@ __device__ __forceinline__ int lp2_r(const float4 (&R)[NU], int n, float radius,
     return fail;
 }
 
+// RVO2 linearProgram3's sub-problem for line i: linearProgram2 over the projections of lines 0..i-1 onto
+// line i (R: lane s holds lines s + 4u), optimising direction (-d.y, d.x) from result = opt * radius.
+// Depends on the lines only. Returns false when it fails (RVO2 then keeps the result it had).
+template <int NU>
+__device__ __forceinline__ bool lp3_sub(const float4 (&R)[NU], const float4 li, int i, float radius, int s, float &rx,
+                                        float &ry)
+{
+    float4 P[NU];
+    uint32_t pv = 0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+        const int j = s + 4 * u;
+        P[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j < i) {
+            bool v;
+            P[u] = proj_line(li, R[u], v);
+            if (v) pv |= 1u << j;
+        }
+    }
+    pv = (uint32_t)quad_or((int)pv);
+    const float ox = -li.w, oy = li.z;   // linearProgram2(projLines, radius, (-d.y, d.x), true)
+    rx = ox * radius; ry = oy * radius;
+    bool fail = false;
+#pragma unroll
+    for (int k = 0; k < 4 * NU; ++k) {
+        if (k < i && !fail && ((pv >> k) & 1u)) {   // quad-uniform
+            const float4 pk = qbc4(P[k >> 2], k);
+            if (det2(pk.z, pk.w, pk.x - rx, pk.y - ry) > 0.0f) {
+                float tL, tR;
+                if (!lp1_r<NU>(P, pv, k, pk, radius, s, tL, tR)) fail = true;
+                else if (ox * pk.z + oy * pk.w > 0.0f) { rx = pk.x + tR * pk.z; ry = pk.y + tR * pk.w; }
+                else { rx = pk.x + tL * pk.z; ry = pk.y + tL * pk.w; }
+            }
+        }
+    }
+    return !fail;
+}
+
 // linearProgram3 from line `begin`; Lb = the same lines in LDS (line i of the outer loop is read from
 // there: its index is dynamic), the projected lines stay in registers (lane s: j = s + 4u)
 template <int NU>
@@ -785,39 +832,81 @@ __device__ __forceinline__ void lp3_r(const float4 (&R)[NU], const float4 *Lb, i
     for (int i = begin; i < n; ++i) {
         const float4 li = Lb[i];
         if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
-            float4 P[NU];
-            uint32_t pv = 0;
-#pragma unroll
-            for (int u = 0; u < NU; ++u) {
-                const int j = s + 4 * u;
-                P[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (j < i) {
-                    bool v;
-                    P[u] = proj_line(li, R[u], v);
-                    if (v) pv |= 1u << j;
-                }
-            }
-            pv = (uint32_t)quad_or((int)pv);
-            const float tx = rx, ty = ry;
-            const float ox = -li.w, oy = li.z;   // linearProgram2(projLines, radius, (-d.y, d.x), true)
-            rx = ox * radius; ry = oy * radius;
-            bool fail = false;
-#pragma unroll
-            for (int k = 0; k < 4 * NU; ++k) {
-                if (k < i && !fail && ((pv >> k) & 1u)) {   // quad-uniform
-                    const float4 pk = qbc4(P[k >> 2], k);
-                    if (det2(pk.z, pk.w, pk.x - rx, pk.y - ry) > 0.0f) {
-                        float tL, tR;
-                        if (!lp1_r<NU>(P, pv, k, pk, radius, s, tL, tR)) fail = true;
-                        else if (ox * pk.z + oy * pk.w > 0.0f) { rx = pk.x + tR * pk.z; ry = pk.y + tR * pk.w; }
-                        else { rx = pk.x + tL * pk.z; ry = pk.y + tL * pk.w; }
-                    }
-                }
-            }
-            if (fail) { rx = tx; ry = ty; }
+            float qx, qy;
+            if (lp3_sub<NU>(R, li, i, radius, s, qx, qy)) { rx = qx; ry = qy; }
             distance = det2(li.z, li.w, li.x - rx, li.y - ry);
         }
     }
+}
+
+// The linearProgram3 sub-problems of a whole workgroup, spread over all its quads (the quad path's step
+// kernel). Sub-problem (h, i) -- human h's line i -- depends on h's lines only, not on the result RVO2's
+// loop has reached when it visits line i, so every one that the loop may visit (i in [fail, n) of each
+// human whose linearProgram2 failed at `fail`) is solved up front, by any quad: sorted by i (descending),
+// so the 16 quads of a wave run sub-problems of about the same size side by side, and one human's
+// sub-problems run on different quads at once. Each human's quad then replays RVO2's loop (lp3_replay).
+// The serial version puts a human's whole loop on its own quad, and the wave runs the union of its 16
+// humans' control flow: for crowded circle crossings that was half of the C2 launch.
+// bn[h] = fail | n << 8 (0: no linearProgram3); results to res / rok [h][12].
+template <int NU>
+__device__ __forceinline__ void lp3_tasks(const float4 *lines, int M, const float *vmax, const uint32_t *bn,
+                                          float2 *res, uint8_t *rok, int tid)
+{
+    const int q = tid >> 2, sq = tid & 3;
+    const uint32_t b = bn[tid & 63];
+    const int b0 = (int)(b & 0xffu), b1 = (int)(b >> 8);
+    uint64_t mk[4 * NU];
+    int cn[4 * NU], T = 0;
+#pragma unroll
+    for (int i = 0; i < 4 * NU; ++i) {   // humans with sub-problem i (wave-uniform)
+        mk[i] = __ballot(b0 <= i && i < b1);
+        cn[i] = __popcll(mk[i]);
+        T += cn[i];
+    }
+    for (int t = q; t < T; t += 64) {   // quad-uniform
+        int i = 0, k = 0, acc = 0;
+        uint64_t m = 0;
+        bool found = false;
+#pragma unroll
+        for (int ii = 4 * NU - 1; ii >= 0; --ii) {
+            if (!found && t < acc + cn[ii]) { found = true; i = ii; k = t - acc; m = mk[ii]; }
+            acc += cn[ii];
+        }
+        for (int z = 0; z < k; ++z) m &= m - 1;   // the k-th human with sub-problem i
+        const int h = __ffsll((long long)m) - 1;
+        const float4 *Lh = lines + h * M;
+        float4 R[NU];
+#pragma unroll
+        for (int u = 0; u < NU; ++u) R[u] = sq + 4 * u < i ? Lh[sq + 4 * u] : make_float4(0.f, 0.f, 0.f, 0.f);
+        float qx, qy;
+        const bool ok = lp3_sub<NU>(R, Lh[i], i, vmax[h], sq, qx, qy);
+        if (sq == 0) { res[h * 12 + i] = make_float2(qx, qy); rok[h * 12 + i] = ok ? 1 : 0; }
+    }
+}
+
+// RVO2's linearProgram3 loop over the sub-problems lp3_tasks solved (lines < `end`), quad-uniform; a visited
+// line >= end has its sub-problem solved here, by the human's own quad (R: its lines, lane s: s + 4u)
+template <int NU>
+__device__ __forceinline__ int lp3_replay(const float4 (&R)[NU], const float4 *Lb, int n, int begin, int end,
+                                          float radius, int s, const float2 *res, const uint8_t *rok, float &rx,
+                                          float &ry)
+{
+    float distance = 0.0f;
+    int vis = 0;
+    for (int i = begin; i < n; ++i) {
+        const float4 li = Lb[i];
+        if (det2(li.z, li.w, li.x - rx, li.y - ry) > distance) {
+            ++vis;
+            if (i < end) {
+                if (rok[i]) { const float2 r2 = res[i]; rx = r2.x; ry = r2.y; }
+            } else {
+                float qx, qy;
+                if (lp3_sub<NU>(R, li, i, radius, s, qx, qy)) { rx = qx; ry = qy; }
+            }
+            distance = det2(li.z, li.w, li.x - rx, li.y - ry);
+        }
+    }
+    return vis;
 }
 
 // one ORCA line (Agent::computeNewVelocity, agent branch) of self vs another agent
@@ -2864,22 +2953,53 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 }
                 wsync();
                 STAMP_A(7);
-                if (hq) {
-                    const float vmq = sl.vmax[h];
-                    float rx, ry;
-                    if constexpr (!KD) {   // <= 12 lines: register-resident linear programs
-                        float4 R[3];
+                if constexpr (!KD) {   // <= 12 lines: register-resident linear programs
+                    uint32_t *l3b = (uint32_t *)(smem + P.o_l3b);
+                    float2 *l3r = (float2 *)(smem + P.o_l3r);
+                    uint8_t *l3k = (uint8_t *)(smem + P.o_l3k);
+                    float rx = 0.0f, ry = 0.0f;
+                    int fail_at = 0;
+                    float4 R[3];
 #pragma unroll
-                        for (int u = 0; u < 3; ++u)
-                            R[u] = sq + 4 * u < cnt ? Lb[sq + 4 * u] : make_float4(0.f, 0.f, 0.f, 0.f);
-                        const int fail_at = lp2_r<3>(R, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
-                        STAMP_A(8);
-                        if (fail_at < cnt) lp3_r<3>(R, Lb, cnt, fail_at, vmq, sq, rx, ry);
-                    } else {
-                        const int fail_at = lp2_q(Lb, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
-                        STAMP_A(8);
-                        if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
+                    for (int u = 0; u < 3; ++u)
+                        R[u] = hq && sq + 4 * u < cnt ? Lb[sq + 4 * u] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (hq) {
+                        fail_at = lp2_r<3>(R, cnt, sl.vmax[h], (float)gdx, (float)gdy, sq, rx, ry);
                     }
+                    STAMP_A(8);
+                    // linearProgram3 of the workgroup's infeasible humans: every sub-problem their loops may
+                    // visit, solved by all quads (lp3_tasks), then each human's quad replays its loop
+                    const bool l3 = hq && fail_at < cnt;
+                    const int l3e = min(cnt, fail_at + CN_LP3_W);
+                    if (sq == 0) l3b[h] = l3 ? (uint32_t)(fail_at | (l3e << 8)) : 0u;
+                    __syncthreads();
+#ifdef CN_STAMPS
+                    const unsigned long long tl3 = clock64();
+#endif
+                    lp3_tasks<3>(sl.lines, M, sl.vmax, l3b, l3r, l3k, tid);
+                    __syncthreads();
+                    int l3vis = 0;
+                    if (l3) l3vis = lp3_replay<3>(R, Lb, cnt, fail_at, l3e, sl.vmax[h], sq, l3r + h * 12, l3k + h * 12, rx, ry);
+#ifdef CN_STAMPS
+                    if (tid == 0 && (unsigned)sb < 4096) cn_stamp_a[sb * CN_NSTAMP + 23] = clock64() - tl3;
+                    if (l3 && sq == 0) {   // sub-problems solved / visited by RVO2's loop
+                        atomicAdd(&cn_lp3_cnt[0], (unsigned long long)(l3e - fail_at));
+                        atomicAdd(&cn_lp3_cnt[1], (unsigned long long)l3vis);
+                    }
+#else
+                    (void)l3vis;
+#endif
+                    STAMP_A(9);
+                    if (hq) {
+                        const bool vr = path_vr_q(h, sq);   // the whole quad
+                        if (sq == 0) human_post(h, (double)rx, (double)ry, vr);
+                    }
+                } else if (hq) {
+                    float rx, ry;
+                    const float vmq = sl.vmax[h];
+                    const int fail_at = lp2_q(Lb, cnt, vmq, (float)gdx, (float)gdy, sq, rx, ry);
+                    STAMP_A(8);
+                    if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
                     STAMP_A(9);
                     const bool vr = path_vr_q(h, sq);   // the whole quad
                     if (sq == 0) human_post(h, (double)rx, (double)ry, vr);
@@ -4077,6 +4197,9 @@ int cn_debug_stamps_r(unsigned long long *r, unsigned long long *sp)
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpyFromSymbol(r, HIP_SYMBOL(cn_stamp_r), sizeof(unsigned long long) * 8192 * 2));
     if (sp) HIPCHK(hipMemcpyFromSymbol(sp, HIP_SYMBOL(cn_stamp_s), sizeof(unsigned long long) * 8192 * 16));
+    unsigned long long l3[14];
+    HIPCHK(hipMemcpyFromSymbol(l3, HIP_SYMBOL(cn_lp3_cnt), sizeof(l3)));
+    for (int k = 0; k < 14; ++k) r[8192 * 2 - 14 + k] = l3[k];   // (the last workgroup slots: never a real grid here)
     return CN_OK;
 }
 

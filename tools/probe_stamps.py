@@ -19,6 +19,8 @@ from crowdnav_dsrnn_amd.engine import CrowdNavEngine  # noqa: E402
 
 
 def run(variant, E=4096, N=10, steps=300):
+    if variant == "c2w":   # the crowded circle centre of bench.py's --steps 20 --warmup 5 window
+        steps = 16
     c = clone_config(Config())
     c.sim.human_num = N
     c.sim.train_val_sim = ["circle_crossing"]
@@ -85,6 +87,8 @@ def run(variant, E=4096, N=10, steps=300):
     L.cn_debug_stamps_r.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     r = np.zeros(8192 * 2, np.uint64)
     L.cn_debug_stamps_r(r.ctypes.data_as(ctypes.c_void_p), None)
+    print("  lp3 sub-problems over all launches: solved %d, visited by RVO2's loop %d" % (int(r[-14]), int(r[-13])))
+    r[-14:] = 0
     R = r.reshape(-1, 2).astype(np.int64)
     live = np.nonzero(R[:, 1] > 0)[0]
     if len(live):
@@ -121,6 +125,9 @@ def run(variant, E=4096, N=10, steps=300):
         sub = [x for x in sub if not x[0].startswith("p0")]
     for nm, v in sub:
         print("      wave0 %-12s median %8d  max %8d" % (nm, np.median(v), v.max()))
+    if variant not in ("c3",):   # linearProgram3 sub-problems of the workgroup (lp3_tasks): count, cycles B1 -> B2
+        cyc = A[:, 23]
+        print("      lp3 task rounds (lp3_tasks + replays) cycles: median %d max %d" % (np.median(cyc), cyc.max()))
     if variant != "c3":   # per-wave ends of phases 0-2 (-DCN_STAMPS lanes 0 / 64 / 128), from the phase start
         per = [("p0 wave1 env load+clip+VR", A[:, 16] - A[:, 0]), ("p1 wave0 visibility", A[:, 19] - A[:, 1]),
                ("p1 wave1 reward terms", A[:, 17] - A[:, 1]), ("p1 wave2 robot terms", A[:, 18] - A[:, 1]),
