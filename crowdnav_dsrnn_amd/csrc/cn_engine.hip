@@ -606,26 +606,24 @@ __device__ __forceinline__ bool lp1_q(const float4 *Lb, MT vmask, int no, float 
     const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
     const float sd = fsqrt(disc);
     float ptl = -INFINITY, ptr = INFINITY;
-    int pf = 0;
     for (int j = s; j < no; j += 4) {
         if (!((vmask >> j) & (MT)1)) continue;
         const float4 li = Lb[j];
         const float den = det2(ln.z, ln.w, li.z, li.w);
         const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
         const bool par = fabsf(den) <= RVO_EPSILON;
-        if (par && num < 0.0f) pf = 1;
         const float t = fdiv(num, den);
         if (!par && den >= 0.0f && t < ptr) ptr = t;
         if (!par && !(den >= 0.0f) && ptl < t) ptl = t;
+        if (par && num < 0.0f) ptl = INFINITY;   // RVO2's parallel-line failure (as in lp1_r)
     }
     ptr = quad_min(ptr);
     ptl = quad_max(ptl);
-    pf = quad_or(pf);
     float tr = -dot + sd, tl = -dot - sd;
     tr = ptr < tr ? ptr : tr;
     tl = tl < ptl ? ptl : tl;
     tL = tl; tR = tr;
-    return !(disc < 0.0f || pf || tl > tr);
+    return !(disc < 0.0f || tl > tr);
 }
 
 // linearProgram2 (optimize closest to (ox, oy)); returns the index of the failing line or n
@@ -730,7 +728,6 @@ __device__ __forceinline__ bool lp1_r(const float4 (&R)[NU], uint32_t vmask, int
     const float disc = dot * dot + radius * radius - (ln.x * ln.x + ln.y * ln.y);
     const float sd = fsqrt(disc);
     float ptl = -INFINITY, ptr = INFINITY;
-    int pf = 0;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
         const int j = s + 4 * u;
@@ -739,20 +736,21 @@ __device__ __forceinline__ bool lp1_r(const float4 (&R)[NU], uint32_t vmask, int
             const float den = det2(ln.z, ln.w, li.z, li.w);
             const float num = det2(li.z, li.w, ln.x - li.x, ln.y - li.y);
             const bool par = fabsf(den) <= RVO_EPSILON;
-            if (par && num < 0.0f) pf = 1;
             const float t = fdiv(num, den);
             if (!par && den >= 0.0f && t < ptr) ptr = t;
             if (!par && !(den >= 0.0f) && ptl < t) ptl = t;
+            // RVO2 fails on a parallel line with numerator < 0: tLeft = +inf (> any tRight, t is finite)
+            // fails the same test below, and rides the max reduction instead of a third quad reduction
+            if (par && num < 0.0f) ptl = INFINITY;
         }
     }
     ptr = quad_min(ptr);
     ptl = quad_max(ptl);
-    pf = quad_or(pf);
     float tr = -dot + sd, tl = -dot - sd;
     tr = ptr < tr ? ptr : tr;
     tl = tl < ptl ? ptl : tl;
     tL = tl; tR = tr;
-    return !(disc < 0.0f || pf || tl > tr);
+    return !(disc < 0.0f || tl > tr);
 }
 
 // linearProgram2 (optimize closest to (ox, oy)) over the n lines of R; returns the failing line or n
