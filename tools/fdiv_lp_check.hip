@@ -1,6 +1,8 @@
-// Check of cn_engine.hip's fdiv_lp (the linear programs' short IEEE division) against the compiler's
-// correctly rounded f32 division, bit for bit, over random operands: numerators with random exponents in
-// [2^-40, 2^40] (and zeros), divisors with |b| in (RVO_EPSILON, 2^40], both signs.
+// Check of cn_engine.hip's fdiv_lp (the linear programs' short IEEE division) and of fsqrt_lp (the same
+// idea for sqrt: exact, but C2-neutral, not kept) against the compiler's correctly rounded f32 division
+// and sqrt, bit for bit: division over random
+// operands (numerators with random exponents in [2^-40, 2^40] and zeros, divisors with |b| in
+// (RVO_EPSILON, 2^40], both signs), sqrt over all 2^32 inputs (NaNs compared as NaN).
 //   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/bin/fdiv_lp_check tools/fdiv_lp_check.hip
 //   tools/bin/fdiv_lp_check [billions]
 #include <hip/hip_runtime.h>
@@ -15,6 +17,29 @@ __device__ __forceinline__ float fdiv_lp(float a, float b)
     const float q0 = a * y1;
     const float q1 = __builtin_fmaf(__builtin_fmaf(-b, q0, a), y1, q0);
     return __builtin_fmaf(__builtin_fmaf(-b, q1, a), y1, q1);
+}
+
+__device__ __forceinline__ float fsqrt_lp(float x)
+{
+    if (__builtin_fabsf(x) < 0x1p-96f && x != 0.0f) return __builtin_sqrtf(x);   // tiny / denormal x: full sequence
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-sd, s, x) <= 0.0f ? sd : s;
+    r = __builtin_fmaf(-su, s, x) > 0.0f ? su : r;
+    return r;
+}
+
+__global__ void check_sqrt(uint64_t base, unsigned long long *bad, float *ex)
+{
+    const uint64_t i = base + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (i > 0xffffffffull) return;
+    const float x = __uint_as_float((uint32_t)i);
+    const float q = __builtin_sqrtf(x), p = fsqrt_lp(x);
+    const bool same = (q != q) ? (p != p) : (__float_as_uint(q) == __float_as_uint(p));
+    if (!same) {
+        const unsigned long long k = atomicAdd(bad, 1ull);
+        if (k < 4) { ex[3 * k] = x; ex[3 * k + 1] = q; ex[3 * k + 2] = p; }
+    }
 }
 
 __device__ __forceinline__ uint32_t mix(uint64_t x)
@@ -54,16 +79,26 @@ int main(int argc, char **argv)
     unsigned long long *bad;
     float *ex;
     if (hipMalloc(&bad, 8) != hipSuccess || hipMalloc(&ex, 48) != hipSuccess) return 2;
-    hipMemset(bad, 0, 8);
+    (void)hipMemset(bad, 0, 8);
     for (uint64_t b0 = 0; b0 < total; b0 += chunk) {
         hipLaunchKernelGGL(check, dim3(16384), dim3(256), 0, 0, b0, total - b0 < chunk ? total - b0 : chunk, bad, ex);
         if (hipDeviceSynchronize() != hipSuccess) return 3;
     }
     unsigned long long h = 0;
     float e[12] = {0};
-    hipMemcpy(&h, bad, 8, hipMemcpyDeviceToHost);
-    hipMemcpy(e, ex, 48, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(&h, bad, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(e, ex, 48, hipMemcpyDeviceToHost);
     printf("fdiv_lp vs IEEE division: %llu mismatches in %.2e pairs\n", h, (double)total);
     for (int k = 0; k < 4 && k < (int)h; ++k) printf("  a=%a b=%a fdiv_lp=%a ieee=%a\n", e[3 * k], e[3 * k + 1], e[3 * k + 2], e[3 * k] / e[3 * k + 1]);
-    return h ? 1 : 0;
+    unsigned long long hs = 0;
+    (void)hipMemset(bad, 0, 8);
+    for (uint64_t b0 = 0; b0 < (1ull << 32); b0 += 256ull * 65536ull) {
+        hipLaunchKernelGGL(check_sqrt, dim3(65536), dim3(256), 0, 0, b0, bad, ex);
+        if (hipDeviceSynchronize() != hipSuccess) return 3;
+    }
+    (void)hipMemcpy(&hs, bad, 8, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(e, ex, 48, hipMemcpyDeviceToHost);
+    printf("fsqrt_lp vs IEEE sqrt: %llu mismatches over all 2^32 inputs\n", hs);
+    for (int k = 0; k < 4 && k < (int)hs; ++k) printf("  x=%a ieee=%a fsqrt_lp=%a\n", e[3 * k], e[3 * k + 1], e[3 * k + 2]);
+    return (h || hs) ? 1 : 0;
 }
