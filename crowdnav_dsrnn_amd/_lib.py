@@ -104,6 +104,8 @@ def lib():
         L.cn_wgrad_work_elems.argtypes = [i64, ctypes.c_int, ctypes.c_int]
         L.cn_wgrad_work_elems.restype = i64
         L.cn_wgrad.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int] + [vp] * 6
+        L.cn_spatial_attn_fwd.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int, ctypes.c_float] + [vp] * 5
+        L.cn_spatial_attn_bwd.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int, ctypes.c_float] + [vp] * 8
     except AttributeError:
         if not os.environ.get("CN_LIB_PATH"):   # an older diagnostic library (A/B runs) may lack them
             raise
@@ -112,7 +114,7 @@ def lib():
                                   ctypes.POINTER(i64)]
     for f in ("cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
               "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features", "cn_profile",
-              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_wgrad", "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict", "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"):
+              "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_spatial_attn_fwd", "cn_spatial_attn_bwd", "cn_wgrad", "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict", "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"):
         if hasattr(L, f) or not os.environ.get("CN_LIB_PATH"):
             getattr(L, f).restype = i32
     _lib = L
@@ -129,7 +131,8 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_destroy", "cn_reset", "cn_step",
             "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
             "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter",
-            "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_wgrad_work_elems", "cn_wgrad",
+            "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_spatial_attn_fwd",
+            "cn_spatial_attn_bwd", "cn_wgrad_work_elems", "cn_wgrad",
             "cn_gru_bias_blocks", "cn_gru_bwd_step_bias", "cn_gru_bias_work_elems", "cn_gru_bias_reduce",
             "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad",
             "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict",

@@ -16,6 +16,7 @@
 // Memory-bound elementwise work: each thread handles 4 consecutive hidden units (16-byte accesses).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <initializer_list>
 
 #include "../../include/crowdnav.h"
 
@@ -562,6 +563,135 @@ __global__ __launch_bounds__(256) void cn_attn_pool_bwd_kernel(int64_t R, int N,
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Whole spatial-edge attention of EdgeAttention.forward (srnn_model.py:256-333) in one pass over hs:
+//   score[r][n] = scale * sum_k te[r][k] (Ws hs[r][n] + bs)[k]  = scale * (hs[r][n] . u[r] + c[r]),
+//   u = te Ws (R x H), c = te . bs (host GEMM / GEMV, R x A x H: 1/10 of the reference's R*N x H x A),
+//   attn = softmax_n(score), out[r] = sum_n attn[r][n] hs[r][n].
+// The reference materialises spatial_embed (R*N x 64), the product with temporal_embed and its sum,
+// then reads hs again for the pooling; here hs is read once (the first 16 of a row's N vectors stay in
+// registers between the score and pooling passes). Same quantity, reassociated (fp32 rounding level).
+// One thread per (row, 4 consecutive h): HQ = H / 4 lanes per row, rows never straddle a wave; the
+// row's scores go through LDS (lane 0 of the row writes, the row's lanes read after a barrier).
+// ------------------------------------------------------------------------------------------------
+#define CN_SA_MAXN 64
+#define CN_SA_REG 16
+
+template <int HQ>
+__global__ __launch_bounds__(256) void cn_spatial_attn_fwd_kernel(int64_t R, int N, float scale,
+                                                                  const float *__restrict__ hs,
+                                                                  const float *__restrict__ u,
+                                                                  const float *__restrict__ c,
+                                                                  float *__restrict__ out, float *__restrict__ attn)
+{
+    constexpr int H = HQ * 4, RB = 256 / HQ;
+    __shared__ float sc[RB][CN_SA_MAXN];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t r = i / HQ;
+    const int q = (int)(i - r * HQ), rl = (int)threadIdx.x / HQ;
+    const bool ok = r < R;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 uu = ok ? *(const float4 *)(u + r * H + q * 4) : z4;
+    const float cr = ok ? c[r] : 0.f;
+    const float *hr = hs + (ok ? r : 0) * (int64_t)N * H + q * 4;
+    float4 vc[CN_SA_REG];
+    float mx = -INFINITY;
+    auto score = [&](int n, const float4 &v) {
+        float part = ((uu.x * v.x + uu.y * v.y) + uu.z * v.z) + uu.w * v.w;
+#pragma unroll
+        for (int o = HQ / 2; o; o >>= 1) part += __shfl_xor(part, o);
+        const float s = (part + cr) * scale;
+        if (q == 0) sc[rl][n] = s;
+        mx = fmaxf(mx, s);
+    };
+#pragma unroll
+    for (int n = 0; n < CN_SA_REG; ++n)
+        if (n < N) {
+            vc[n] = ok ? *(const float4 *)(hr + n * H) : z4;
+            score(n, vc[n]);
+        }
+    for (int n = CN_SA_REG; n < N; ++n) score(n, ok ? *(const float4 *)(hr + n * H) : z4);
+    __syncthreads();
+    float den = 0.f;
+    for (int n = 0; n < N; ++n) den += expf(sc[rl][n] - mx);
+    float4 acc = z4;
+    auto pool = [&](int n, const float4 &v) {
+        const float a = expf(sc[rl][n] - mx) / den;
+        acc.x += v.x * a; acc.y += v.y * a; acc.z += v.z * a; acc.w += v.w * a;
+        if (ok && q == 0) attn[r * N + n] = a;
+    };
+#pragma unroll
+    for (int n = 0; n < CN_SA_REG; ++n)
+        if (n < N) pool(n, vc[n]);
+    for (int n = CN_SA_REG; n < N; ++n) pool(n, ok ? *(const float4 *)(hr + n * H) : z4);
+    if (ok) *(float4 *)(out + r * H + q * 4) = acc;
+}
+
+// Gradient: p[n] = dout[r] . hs[r][n] (+ the caller's d attn), s = sum_n attn[n] p[n],
+// dscore[n] = scale * attn[n] (p[n] - s) (softmax backward), then
+//   dhs[r][n] = attn[n] dout[r] + dscore[n] u[r],  du[r] = sum_n dscore[n] hs[r][n],  dc[r] = sum_n dscore[n].
+// hs is read once (as forward); dhs written once (it is the spatial GRU output's whole gradient).
+template <int HQ>
+__global__ __launch_bounds__(256) void cn_spatial_attn_bwd_kernel(int64_t R, int N, float scale,
+                                                                  const float *__restrict__ hs,
+                                                                  const float *__restrict__ u,
+                                                                  const float *__restrict__ attn,
+                                                                  const float *__restrict__ dout,
+                                                                  const float *__restrict__ dattn,
+                                                                  float *__restrict__ dhs, float *__restrict__ du,
+                                                                  float *__restrict__ dc)
+{
+    constexpr int H = HQ * 4, RB = 256 / HQ;
+    __shared__ float sp[RB][CN_SA_MAXN];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t r = i / HQ;
+    const int q = (int)(i - r * HQ), rl = (int)threadIdx.x / HQ;
+    const bool ok = r < R;
+    const int64_t rr = ok ? r : 0;
+    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 g = ok ? *(const float4 *)(dout + r * H + q * 4) : z4;
+    const float4 uu = ok ? *(const float4 *)(u + r * H + q * 4) : z4;
+    const float *hr = hs + rr * (int64_t)N * H + q * 4;
+    float4 vc[CN_SA_REG];
+    float s = 0.f;
+    auto grad = [&](int n, const float4 &v) {
+        float part = ((g.x * v.x + g.y * v.y) + g.z * v.z) + g.w * v.w;
+#pragma unroll
+        for (int o = HQ / 2; o; o >>= 1) part += __shfl_xor(part, o);
+        if (dattn) part += dattn[rr * N + n];
+        if (q == 0) sp[rl][n] = part;
+        s += attn[rr * N + n] * part;
+    };
+#pragma unroll
+    for (int n = 0; n < CN_SA_REG; ++n)
+        if (n < N) {
+            vc[n] = ok ? *(const float4 *)(hr + n * H) : z4;
+            grad(n, vc[n]);
+        }
+    for (int n = CN_SA_REG; n < N; ++n) grad(n, ok ? *(const float4 *)(hr + n * H) : z4);
+    __syncthreads();
+    float4 acc = z4;
+    float dcs = 0.f;
+    float *dr = dhs + rr * (int64_t)N * H + q * 4;
+    auto back = [&](int n, const float4 &v) {
+        const float a = attn[rr * N + n];
+        const float ds = scale * (a * (sp[rl][n] - s));
+        acc.x += ds * v.x; acc.y += ds * v.y; acc.z += ds * v.z; acc.w += ds * v.w;
+        dcs += ds;
+        if (ok)
+            *(float4 *)(dr + n * H) = make_float4(a * g.x + ds * uu.x, a * g.y + ds * uu.y, a * g.z + ds * uu.z,
+                                                  a * g.w + ds * uu.w);
+    };
+#pragma unroll
+    for (int n = 0; n < CN_SA_REG; ++n)
+        if (n < N) back(n, vc[n]);
+    for (int n = CN_SA_REG; n < N; ++n) back(n, ok ? *(const float4 *)(hr + n * H) : z4);
+    if (ok) {
+        *(float4 *)(du + r * H + q * 4) = acc;
+        if (q == 0) dc[r] = dcs;
+    }
+}
+
 
 // ------------------------------------------------------------------------------------------------
 // Skinny weight gradient of a Linear layer applied to K >> 1 rows (PPO minibatch: T*B or T*B*N rows):
@@ -782,6 +912,60 @@ int cn_attn_pool_bwd(void *stream, int64_t R, int N, int H, const float *hs, con
     else
         hipLaunchKernelGGL(cn_attn_pool_bwd_kernel<16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, hs, attn,
                            dout, dhs, dattn);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+static int sa_check(const char *who, int64_t R, int N, int H, std::initializer_list<const void *> vec,
+                    std::initializer_list<const void *> other)
+{
+    if (R <= 0 || N <= 0 || N > CN_SA_MAXN || !(H == 256 || H == 128 || H == 64))
+        return cn_set_error(CN_EINVAL, who);
+    for (const void *p : vec)
+        if (!p || ((uintptr_t)p & 15)) return cn_set_error(CN_EINVAL, who);
+    for (const void *p : other)
+        if (!p) return cn_set_error(CN_EINVAL, who);
+    return CN_OK;
+}
+
+int cn_spatial_attn_fwd(void *stream, int64_t R, int N, int H, float scale, const float *hs, const float *u,
+                        const float *c, float *out, float *attn)
+{
+    if (sa_check("cn_spatial_attn_fwd: H in {64, 128, 256}, 1 <= N <= 64, non-null operands, hs / u / out "
+                 "16-byte aligned", R, N, H, {hs, u, out}, {c, attn}))
+        return CN_EINVAL;
+    const unsigned grid = grid_for(R, H);
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
+    if (H == 256)
+        hipLaunchKernelGGL(cn_spatial_attn_fwd_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
+                           hs, u, c, out, attn);
+    else if (H == 128)
+        hipLaunchKernelGGL(cn_spatial_attn_fwd_kernel<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
+                           hs, u, c, out, attn);
+    else
+        hipLaunchKernelGGL(cn_spatial_attn_fwd_kernel<16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
+                           hs, u, c, out, attn);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+int cn_spatial_attn_bwd(void *stream, int64_t R, int N, int H, float scale, const float *hs, const float *u,
+                        const float *attn, const float *dout, const float *dattn, float *dhs, float *du, float *dc)
+{
+    if (sa_check("cn_spatial_attn_bwd: H in {64, 128, 256}, 1 <= N <= 64, non-null operands, hs / u / dout / "
+                 "dhs / du 16-byte aligned", R, N, H, {hs, u, dout, dhs, du}, {attn, dc}))
+        return CN_EINVAL;
+    const unsigned grid = grid_for(R, H);
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
+    if (H == 256)
+        hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
+                           hs, u, attn, dout, dattn, dhs, du, dc);
+    else if (H == 128)
+        hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
+                           hs, u, attn, dout, dattn, dhs, du, dc);
+    else
+        hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
+                           hs, u, attn, dout, dattn, dhs, du, dc);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }

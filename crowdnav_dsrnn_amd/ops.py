@@ -336,3 +336,56 @@ def attention_pool(hs, attn):
         raise EdgeFeaturesUnavailable("the DSRNN attention pooling runs only as the HIP kernel (cn_attn_pool_*); "
                                       "tensors are on %s" % hs.device)
     return _AttnPool.apply(hs, attn)
+
+
+class _SpatialAttn(torch.autograd.Function):
+    """srnn_model.py:256-333 (EdgeAttention.att_func + the bmm pooling) for the spatial edges, with the
+    spatial_edge_layer folded into the score: score = scale * (hs . (te Ws) + te . bs), the same quantity
+    as scale * sum_k te_k (Ws hs + bs)_k reassociated, so the (R*N, 64) spatial embedding, its product with
+    temporal_embed and the second read of hs for the pooling are never formed (cn_spatial_attn_fwd: one
+    pass over hs). Backward: cn_spatial_attn_bwd (one pass: dhs, du, dc), then the small host GEMMs
+    d te = du Ws^T + dc bs^T, dWs = te^T du, dbs = te^T dc."""
+
+    @staticmethod
+    def forward(ctx, hs, te, ws, bs, scale):
+        R, N, H = hs.shape
+        hs, te = _c(hs), _c(te)
+        u = torch.mm(te, ws)                 # (R, H)
+        c = torch.mv(te, bs)                 # (R,)
+        out = torch.empty((R, H), dtype=torch.float32, device=hs.device)
+        attn = torch.empty((R, N), dtype=torch.float32, device=hs.device)
+        with torch.cuda.device(hs.device):
+            _lib.check(_lib.lib().cn_spatial_attn_fwd(_stream(hs.device), R, N, H, float(scale), hs.data_ptr(),
+                                                      u.data_ptr(), c.data_ptr(), out.data_ptr(), attn.data_ptr()))
+        ctx.scale = float(scale)
+        ctx.save_for_backward(hs, te, ws, bs, u, attn)
+        return out, attn.reshape(R, N, 1)
+
+    @staticmethod
+    def backward(ctx, dout, dattn):
+        hs, te, ws, bs, u, attn = ctx.saved_tensors
+        R, N, H = hs.shape
+        dev = hs.device
+        dout = _c(dout) if dout is not None else torch.zeros((R, H), dtype=torch.float32, device=dev)
+        da = _c(dattn).reshape(R, N) if dattn is not None else None
+        dhs = torch.empty_like(hs)
+        du = torch.empty((R, H), dtype=torch.float32, device=dev)
+        dc = torch.empty((R,), dtype=torch.float32, device=dev)
+        with torch.cuda.device(dev):
+            _lib.check(_lib.lib().cn_spatial_attn_bwd(_stream(dev), R, N, H, ctx.scale, hs.data_ptr(), u.data_ptr(),
+                                                      attn.data_ptr(), dout.data_ptr(),
+                                                      da.data_ptr() if da is not None else None, dhs.data_ptr(),
+                                                      du.data_ptr(), dc.data_ptr()))
+        dte = torch.addmm(torch.outer(dc, bs), du, ws.t()) if ctx.needs_input_grad[1] else None
+        dws = torch.mm(te.t(), du) if ctx.needs_input_grad[2] else None
+        dbs = torch.mv(te.t(), dc) if ctx.needs_input_grad[3] else None
+        return dhs, dte, dws, dbs, None
+
+
+def spatial_attention(hs, te, ws, bs, scale):
+    """hs (R, N, H) spatial edge states, te (R, A) temporal_embed, ws (A, H) / bs (A,) spatial_edge_layer
+    -> weighted (R, H), attn (R, N, 1) of EdgeAttention (srnn_model.py:256-333), one HIP pass over hs."""
+    if not hs.is_cuda:
+        raise EdgeFeaturesUnavailable("the DSRNN spatial attention runs only as the HIP kernel (cn_spatial_attn_*); "
+                                      "tensors are on %s" % hs.device)
+    return _SpatialAttn.apply(hs, te, ws, bs, scale)

@@ -113,9 +113,16 @@ class EdgeAttention(nn.Module):
         """h_temporal (T,B,256), h_spatials (T,B,N,256) -> weighted (T,B,256), attn (T*B,N,1)."""
         T, B, N, H = h_spatials.shape
         temporal_embed = self.temporal_edge_layer[0](h_temporal)          # (T,B,64)
+        scale = N / np.sqrt(self.attention_size)                          # temperature = num_edges / sqrt(d)
+        if h_spatials.is_cuda and H in (64, 128, 256) and N <= 64:
+            # spatial_edge_layer, scores, softmax and pooling in one pass over h_spatials (ops.spatial_attention)
+            sl = self.spatial_edge_layer[0]
+            weighted, attn = ops.spatial_attention(h_spatials.reshape(T * B, N, H), temporal_embed.reshape(T * B, -1),
+                                                   sl.weight, sl.bias, scale)
+            return weighted.reshape(T, B, H), attn
         spatial_embed = self.spatial_edge_layer[0](h_spatials)            # (T,B,N,64)
         attn = (spatial_embed * temporal_embed.unsqueeze(2)).sum(-1)      # (T,B,N)
-        attn = attn * (N / np.sqrt(self.attention_size))                  # temperature = num_edges / sqrt(d)
+        attn = attn * scale
         attn = torch.softmax(attn, dim=-1).reshape(T * B, N, 1)
         weighted = ops.attention_pool(h_spatials.reshape(T * B, N, H), attn)  # bmm(hs^T, attn): (T*B, H)
         return weighted.reshape(T, B, H), attn

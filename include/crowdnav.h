@@ -31,6 +31,9 @@
  *   cn_wgrad       ⟵ the weight / bias gradient of the Linear layers with a tiny side (autograd's dy^T x)
  *   cn_attn_pool_fwd / cn_attn_pool_bwd ⟵ EdgeAttention's weighted sum of the spatial edge states
  *                   (srnn_model.py:320-333, torch.bmm(h_spatials^T, attn)) and its gradient
+ *   cn_spatial_attn_fwd / cn_spatial_attn_bwd ⟵ EdgeAttention's whole spatial branch (spatial_edge_layer,
+ *                   att_func's scores and softmax, the pooling: srnn_model.py:256-333) in one pass over
+ *                   h_spatials, and its gradient (the training and act() paths use these)
  *
  * Conventions
  *   - All array arguments are DEVICE pointers (torch tensors' data_ptr()), row-major, caller-owned.
@@ -339,6 +342,21 @@ int cn_attn_pool_fwd(void *stream, int64_t R, int N, int H, const float *hs, con
  * dattn[r][n] = sum_h dout[r][h] * hs[r][n][h] (fixed-order reduction). H in {64, 128, 256}. */
 int cn_attn_pool_bwd(void *stream, int64_t R, int N, int H, const float *hs, const float *attn, const float *dout,
                      float *dhs, float *dattn);
+
+/* The whole spatial-edge attention of EdgeAttention.forward (srnn_model.py:256-333: spatial_edge_layer,
+ * the product with temporal_embed summed over the embedding, * num_edges / sqrt(attention_size), softmax
+ * over the N edges, bmm pooling) in one pass over hs, given u = temporal_embed @ Ws [R][H] and
+ * c = temporal_embed . bs [R] from the caller (Ws, bs: spatial_edge_layer's weight [A][H] and bias [A]):
+ *   attn[r][n] = softmax_n(scale * (hs[r][n] . u[r] + c[r])),  out[r] = sum_n attn[r][n] hs[r][n].
+ * hs [R][N][H], out [R][H], attn [R][N]; H in {64, 128, 256}, 1 <= N <= 64; hs, u, out 16-byte aligned. */
+int cn_spatial_attn_fwd(void *stream, int64_t R, int N, int H, float scale, const float *hs, const float *u,
+                        const float *c, float *out, float *attn);
+
+/* Gradient of cn_spatial_attn_fwd given dout [R][H] and optionally dattn [R][N] (null: none):
+ * dhs [R][N][H], du [R][H] (-> d temporal_embed = du Ws^T + dc bs^T, dWs = temporal_embed^T du on the
+ * caller's side), dc [R]. hs, u, dout, dhs, du 16-byte aligned. */
+int cn_spatial_attn_bwd(void *stream, int64_t R, int N, int H, float scale, const float *hs, const float *u,
+                        const float *attn, const float *dout, const float *dattn, float *dhs, float *du, float *dc);
 
 /* Weight gradient of a Linear layer over K rows with a tiny side (ops.linear / the fused input layers'
  * backward, replacing torch's dy^T x in the reference's autograd of srnn_model.py:160-161,210-211,466 and

@@ -238,6 +238,56 @@ def test_attention_pool_kernels_vs_fp64(R, N, H):
         np.testing.assert_allclose(a.numpy(), b.numpy(), atol=1e-5 * max(1.0, float(b.abs().max())), rtol=0, err_msg=n)
 
 
+def spatial_attention_ref(hs, te, ws, bs, scale):
+    """EdgeAttention's spatial branch as the reference writes it (srnn_model.py:256-333): spatial_edge_layer,
+    product with temporal_embed summed over the embedding, * scale, softmax over the edges, bmm pooling."""
+    se = hs @ ws.t() + bs                                   # (R, N, A)
+    attn = torch.softmax((se * te.unsqueeze(1)).sum(-1) * scale, -1).unsqueeze(-1)
+    return torch.bmm(hs.transpose(1, 2), attn).squeeze(-1), attn
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,N,H", [(1, 1, 256), (37, 10, 256), (300, 25, 128), (5, 3, 64), (4099, 20, 256),
+                                   (9, 64, 64)])
+def test_spatial_attention_kernels_vs_fp64(R, N, H):
+    """cn_spatial_attn_fwd / _bwd (spatial_edge_layer folded into the score: reassociated) vs the
+    reference's composition in float64: output, attention and the gradients of h_spatials, temporal_embed,
+    the layer's weight and bias, with a gradient arriving on the returned attention too (N > 16 covers the
+    reloaded tail of a row). fp32 accumulation over H and N: atol 2e-5 x scale."""
+    from crowdnav_dsrnn_amd import ops
+
+    A = 64
+    g = torch.Generator().manual_seed(R * 11 + N)
+    hs = torch.randn(R, N, H, generator=g)
+    te = torch.relu(torch.randn(R, A, generator=g)) * 0.3
+    ws = torch.randn(A, H, generator=g) / 16
+    bs = torch.randn(A, generator=g) * 0.1
+    dout = torch.randn(R, H, generator=g)
+    datt = torch.randn(R, N, 1, generator=g)
+    scale = N / np.sqrt(A)
+
+    def run(fn, dev, dt):
+        xs = [t.to(dev, dt).requires_grad_(True) for t in (hs, te, ws, bs)]
+        out, att = fn(*xs, scale)
+        ((out * dout.to(dev, dt)).sum() + (att * datt.to(dev, dt)).sum()).backward()
+        return [x.detach().cpu().double() for x in [out, att] + [t.grad for t in xs]]
+
+    got = run(ops.spatial_attention, "cuda:0", torch.float32)
+    want = run(spatial_attention_ref, "cpu", torch.float64)
+    for n, a, b in zip(("out", "attn", "d_hs", "d_te", "d_ws", "d_bs"), got, want):
+        tol = 2e-5 * max(1.0, float(b.abs().max())) * (max(1.0, R / 256) if n in ("d_ws", "d_bs") else 1.0)
+        np.testing.assert_allclose(a.numpy(), b.numpy(), atol=tol, rtol=0, err_msg=n)
+
+
+@pytest.mark.gpu
+def test_spatial_attention_rejects_bad_shapes():
+    from crowdnav_dsrnn_amd import _lib
+
+    L = _lib.lib()
+    assert L.cn_spatial_attn_fwd(None, 4, 65, 256, 1.0, None, None, None, None, None) != 0   # N > 64
+    assert L.cn_spatial_attn_fwd(None, 4, 10, 96, 1.0, None, None, None, None, None) != 0    # H not 64/128/256
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,H,G", [(20480, 256, 10), (4099, 128, 1), (1, 256, 1), (130, 64, 5)])
 def test_gru_fused_step_vs_gemm_plus_gates(B, H, G):
