@@ -73,14 +73,18 @@ def build(force=False, verbose=False):
     tmp = LIB_PATH + ".tmp%d" % os.getpid()
     objs = []
     try:
-        for src in SOURCES:   # one object per source (its own flags), then one shared link
+        procs = []
+        for src in SOURCES:   # one object per source (its own flags), compiled side by side, then one link
             obj = "%s.%s.o" % (tmp, os.path.basename(src))
             cmd = ([hipcc(), "--offload-arch=" + ARCH] + FLAGS + SRC_FLAGS.get(os.path.basename(src), []) +
                    ['-DCN_SRC_HASH="%s"' % source_hash(), "-c", "-o", obj, src])
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
-            subprocess.run(cmd, check=True)
+            procs.append((subprocess.Popen(cmd), cmd))
             objs.append(obj)
+        failed = [cmd for p, cmd in procs if p.wait() != 0]
+        if failed:
+            raise subprocess.CalledProcessError(1, failed[0])
         cmd = [hipcc(), "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs
         if verbose:
             print(" ".join(cmd), file=sys.stderr)

@@ -275,7 +275,10 @@ def test_spatial_attention_kernels_vs_fp64(R, N, H):
     got = run(ops.spatial_attention, "cuda:0", torch.float32)
     want = run(spatial_attention_ref, "cpu", torch.float64)
     for n, a, b in zip(("out", "attn", "d_hs", "d_te", "d_ws", "d_bs"), got, want):
-        tol = 2e-5 * max(1.0, float(b.abs().max())) * (max(1.0, R / 256) if n in ("d_ws", "d_bs") else 1.0)
+        # d_bs is exactly 0 in exact arithmetic (te . bs shifts a row's scores uniformly; softmax ignores it):
+        # both fp32 implementations return rounding noise of sums of te * dscore terms, which d_ws bounds
+        ref = want[4] if n == "d_bs" else b
+        tol = 2e-5 * max(1.0, float(ref.abs().max())) * (max(1.0, R / 256) if n in ("d_ws", "d_bs") else 1.0)
         np.testing.assert_allclose(a.numpy(), b.numpy(), atol=tol, rtol=0, err_msg=n)
 
 
