@@ -262,7 +262,9 @@ def gru_gemm_roofline(torch, device, B, H, reps=50):
 def dsrnn_flop_per_env_step(N, c):
     """Algorithmic forward FLOP of the DSRNN policy per env-step (srnn_model.py:409-504 with the config's
     sizes): 2*M*K per output of every Linear / GRU gate GEMM (gi and gh), attention scores and pooling;
-    the elementwise gate / activation arithmetic is not counted. 6.63 MFLOP at N = 10."""
+    the elementwise gate / activation arithmetic is not counted. 6.63 MFLOP at N = 10. This is the
+    reference's algorithm: ops.spatial_attention reassociates the spatial_edge_layer term (2*He*A*N of `att`,
+    0.33 MFLOP at N = 10) into 2*A*He + 2*He*N, so ~5 % of the count is no longer executed."""
     S = c.SRNN
     He, Hn, emb = S.human_human_edge_rnn_size, S.human_node_rnn_size, S.human_human_edge_embedding_size
     enc = 2 * 2 * emb * (N + 1) + 2 * 7 * 3 + 2 * 3 * S.human_node_embedding_size
