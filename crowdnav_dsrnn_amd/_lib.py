@@ -105,7 +105,7 @@ def lib():
         L.cn_wgrad_work_elems.restype = i64
         L.cn_wgrad.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int] + [vp] * 6
         L.cn_spatial_attn_fwd.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int, ctypes.c_float] + [vp] * 5
-        L.cn_spatial_attn_bwd.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int, ctypes.c_float] + [vp] * 8
+        L.cn_spatial_attn_bwd.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int, ctypes.c_float] + [vp] * 7 + [i64, vp, i64]
     except AttributeError:
         if not os.environ.get("CN_LIB_PATH"):   # an older diagnostic library (A/B runs) may lack them
             raise

@@ -639,7 +639,7 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_bwd_kernel(int64_t R, int
                                                                   const float *__restrict__ dout,
                                                                   const float *__restrict__ dattn,
                                                                   float *__restrict__ dhs, float *__restrict__ du,
-                                                                  float *__restrict__ dc)
+                                                                  int64_t ldu, float *__restrict__ dc, int64_t ldc)
 {
     constexpr int H = HQ * 4, RB = 256 / HQ;
     __shared__ float sp[RB][CN_SA_MAXN];
@@ -687,8 +687,8 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_bwd_kernel(int64_t R, int
         if (n < N) back(n, vc[n]);
     for (int n = CN_SA_REG; n < N; ++n) back(n, ok ? *(const float4 *)(hr + n * H) : z4);
     if (ok) {
-        *(float4 *)(du + r * H + q * 4) = acc;
-        if (q == 0) dc[r] = dcs;
+        *(float4 *)(du + r * ldu + q * 4) = acc;
+        if (q == 0) dc[r * ldc] = dcs;
     }
 }
 
@@ -950,22 +950,24 @@ int cn_spatial_attn_fwd(void *stream, int64_t R, int N, int H, float scale, cons
 }
 
 int cn_spatial_attn_bwd(void *stream, int64_t R, int N, int H, float scale, const float *hs, const float *u,
-                        const float *attn, const float *dout, const float *dattn, float *dhs, float *du, float *dc)
+                        const float *attn, const float *dout, const float *dattn, float *dhs, float *du, int64_t ldu,
+                        float *dc, int64_t ldc)
 {
     if (sa_check("cn_spatial_attn_bwd: H in {64, 128, 256}, 1 <= N <= 64, non-null operands, hs / u / dout / "
-                 "dhs / du 16-byte aligned", R, N, H, {hs, u, dout, dhs, du}, {attn, dc}))
-        return CN_EINVAL;
+                 "dhs / du 16-byte aligned, ldu >= H and a multiple of 4, ldc >= 1", R, N, H, {hs, u, dout, dhs, du},
+                 {attn, dc}) || ldu < H || (ldu & 3) || ldc < 1)
+        return cn_set_error(CN_EINVAL, "cn_spatial_attn_bwd: bad shape, stride or operand");
     const unsigned grid = grid_for(R, H);
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     if (H == 256)
         hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, attn, dout, dattn, dhs, du, dc);
+                           hs, u, attn, dout, dattn, dhs, du, ldu, dc, ldc);
     else if (H == 128)
         hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, attn, dout, dattn, dhs, du, dc);
+                           hs, u, attn, dout, dattn, dhs, du, ldu, dc, ldc);
     else
         hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, attn, dout, dattn, dhs, du, dc);
+                           hs, u, attn, dout, dattn, dhs, du, ldu, dc, ldc);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }

@@ -369,16 +369,19 @@ class _SpatialAttn(torch.autograd.Function):
         dout = _c(dout) if dout is not None else torch.zeros((R, H), dtype=torch.float32, device=dev)
         da = _c(dattn).reshape(R, N) if dattn is not None else None
         dhs = torch.empty_like(hs)
-        du = torch.empty((R, H), dtype=torch.float32, device=dev)
-        dc = torch.empty((R,), dtype=torch.float32, device=dev)
+        ld = H + 4                           # [du | dc | pad] rows: dWs and dbs from one split-K GEMM
+        due = torch.empty((R, ld), dtype=torch.float32, device=dev)
+        du, dc = due[:, :H], due[:, H]
         with torch.cuda.device(dev):
             _lib.check(_lib.lib().cn_spatial_attn_bwd(_stream(dev), R, N, H, ctx.scale, hs.data_ptr(), u.data_ptr(),
                                                       attn.data_ptr(), dout.data_ptr(),
                                                       da.data_ptr() if da is not None else None, dhs.data_ptr(),
-                                                      du.data_ptr(), dc.data_ptr()))
+                                                      due.data_ptr(), ld, due.data_ptr() + 4 * H, ld))
         dte = torch.addmm(torch.outer(dc, bs), du, ws.t()) if ctx.needs_input_grad[1] else None
-        dws = torch.mm(te.t(), du) if ctx.needs_input_grad[2] else None
-        dbs = torch.mv(te.t(), dc) if ctx.needs_input_grad[3] else None
+        dws = dbs = None
+        if ctx.needs_input_grad[2] or ctx.needs_input_grad[3]:
+            g = wgrad(te, due)               # (A, H + 4) = te^T [du | dc | pad]; the pad columns are dropped
+            dws, dbs = g[:, :H].contiguous(), g[:, H].contiguous()
         return dhs, dte, dws, dbs, None
 
 

@@ -353,10 +353,12 @@ int cn_spatial_attn_fwd(void *stream, int64_t R, int N, int H, float scale, cons
                         const float *c, float *out, float *attn);
 
 /* Gradient of cn_spatial_attn_fwd given dout [R][H] and optionally dattn [R][N] (null: none):
- * dhs [R][N][H], du [R][H] (-> d temporal_embed = du Ws^T + dc bs^T, dWs = temporal_embed^T du on the
- * caller's side), dc [R]. hs, u, dout, dhs, du 16-byte aligned. */
+ * dhs [R][N][H], du rows of H at stride ldu (-> d temporal_embed = du Ws^T + dc bs^T, dWs = temporal_embed^T du
+ * on the caller's side), dc at stride ldc (dc = du + H with ldc = ldu puts [du | dc] in one matrix, so
+ * dWs and dbs come from one GEMM). hs, u, dout, dhs, du 16-byte aligned; ldu >= H, ldu % 4 == 0. */
 int cn_spatial_attn_bwd(void *stream, int64_t R, int N, int H, float scale, const float *hs, const float *u,
-                        const float *attn, const float *dout, const float *dattn, float *dhs, float *du, float *dc);
+                        const float *attn, const float *dout, const float *dattn, float *dhs, float *du, int64_t ldu,
+                        float *dc, int64_t ldc);
 
 /* Weight gradient of a Linear layer over K rows with a tiny side (ops.linear / the fused input layers'
  * backward, replacing torch's dy^T x in the reference's autograd of srnn_model.py:160-161,210-211,466 and
