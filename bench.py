@@ -4,6 +4,11 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`python bench.py --gpus N` (N > 1) without WORLD_SIZE launches the N rank processes itself (a child
+torch.distributed.run on 127.0.0.1, before this process touches the GPU) and exits with its code -- the
+reference builds its whole worker pool from one make_vec_envs call (envs.py:120-139). Under a launcher,
+--gpus must equal WORLD_SIZE.
+
 Workload (BASELINE.json configs[1]): per GPU 4096 envs x 10 humans, circle_crossing,
 ORCA humans, unicycle robot, dt = 0.25, reference config defaults (randomize_attributes, goal
 changing, auto-reset). A "step" is one cn_step of every env: clip_action, ORCA for every human,
@@ -12,7 +17,11 @@ U[-0.1, 0.1]^2 (dv, dtheta), generated on the device (torch Philox, seed = rank)
 region, so the timed region only runs the env hot path with inputs resident in HBM.
 Multi-GPU: envs shard with no collective (env g of rank r is global env r*E+g; thisSeed/nenv are
 global) -> weak scaling; timing = max over ranks between barriers.
-One JSON line on rank 0 (bench contract in the task statement).
+One JSON line on rank 0 (bench contract in the task statement). The main window is the K launches after
+W warm-up launches after cn_reset (the driver's --steps 20 --warmup 5: launches 6-25 of the first
+episodes, few auto-resets); `steady_state` in the same line is SURVEY §8d's window on the same engine:
+100 more warm-up launches, then 2,000 timed ones including all their auto-resets (`resets` = episodes
+ended and restarted inside the window, counted from the engine's per-env reset counters).
 """
 import argparse
 import ctypes
@@ -33,7 +42,7 @@ WORKLOAD_DESC = {
     "c3": "C3: %d envs/GPU x %d humans, square_crossing, robot/human FOV pi, ORCA humans (kd-tree path), "
           "holonomic robot, actions N(0,0.5^2), auto-reset",
     "c4": "C4: %d envs/GPU x %d humans, circle_crossing, ORCA humans, holonomic robot, DSRNN act() in the loop "
-          "(sampled actions), PPO num_steps=128 epochs=5 minibatches=2, grads all-reduced over RCCL",
+          "(sampled actions), PPO num_steps=128 epochs=5 minibatches=2",
     "c5": "C5: %d envs/GPU in ONE mixed engine, per-env scenario dispatch round-robin over parallel / "
           "perpendicular traffic (%s humans) and the 3 side_pref scenarios (1 human, padded), norm-zone reward, "
           "holonomic, ORCA",
@@ -167,11 +176,13 @@ def cpu_baseline(N, budget_s=12.0):
     return out
 
 
-def load_pmc(kernel="cn_step_kernel", workload="c2"):
+def load_pmc(kernel="cn_step_kernel", workload="c2", window=None):
     """Counter figures for `kernel` from the newest committed rocprofv3 summary (profiles/pmc_<tag>.json,
     written by profiles/summarize.py) that was measured on a library built from EXACTLY the sources this
     run uses (CN_SRC_HASH) and on the same workload; None when no such profile exists (a stale profile
-    is never reported)."""
+    is never reported). window = (first, count): the figures of exactly those launches after cn_reset
+    (0-based first launch), which the profile must have split out (summarize.py `windows`); a profile of
+    another window is not reported for this one."""
     import glob
 
     from crowdnav_dsrnn_amd import build
@@ -192,7 +203,13 @@ def load_pmc(kernel="cn_step_kernel", workload="c2"):
         if wl != workload:
             continue
         for k, d in doc.get("kernels", {}).items():
-            if kernel in k and "hbm_bytes_per_launch" in d:
+            if kernel not in k:
+                continue
+            if window is not None:
+                d = next((w for w in d.get("windows", []) if (w.get("first"), w.get("count")) == tuple(window)), None)
+                if d is None:
+                    continue
+            if "hbm_bytes_per_launch" in d:
                 if best is None or os.path.getmtime(p) > best[0]:
                     best = (os.path.getmtime(p), doc["tag"], d)
     if best is None:
@@ -368,16 +385,76 @@ def run_c4(args, torch, dist, device, rank, world):
             "unit": "env-steps/s", "n_gpus": world, "steps": K, "warmup": W,
             "ms_per_step": round(elapsed / K * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f64 env / fp32 policy", "data": "synthetic",
-            "config": {"workload": WORKLOAD_DESC["c4"] % (E, N), "envs_per_gpu": E, "humans": N,
+            "config": {"workload": WORKLOAD_DESC["c4"] % (E, N) + (", grads all-reduced over RCCL" if world > 1 else ""),
+                       "envs_per_gpu": E, "humans": N,
                        "global_envs": E * world, "env_steps_per_update": steps_per_update * world,
                        "rollout_s_per_update": round(roll / K, 4), "ppo_s_per_update": round(upd / K, 4),
-                       "parallelism": "dp%d (env-sharded, PPO grads all-reduced)" % world},
+                       "rollout_timing": "HIP events on the update's stream (rollout = act + cn_step + storage, "
+                                         "incl. get_value / compute_returns; ppo = PPO.update)",
+                       "parallelism": "dp%d (env-sharded%s)" % (world, ", PPO grads all-reduced" if world > 1 else "")},
             "roofline": roof,
             "whole_update_roofline": whole,
         }
         print(json.dumps(line), flush=True)
     envs.close()
     if dist is not None:
+        dist.destroy_process_group()
+
+
+def reset_total(eng):
+    """Sum over envs of the engine's per-env reset counter (state field reset_count: one per auto-reset
+    inside cn_step, crowd_sim_dict.py:105 via shmem_vec_env.py:166-167). Host copy of the state, outside
+    any timed region."""
+    st = eng.get_state()
+    views = [v for _, v in st] if isinstance(st, list) else [st]
+    return int(sum(int(v.reset_count.astype(np.int64).sum()) for v in views))
+
+
+def launch_plan(gpus, environ):
+    """How this invocation runs: ("run", world) inside a launcher (or a plain 1-GPU run), ("spawn", N) when
+    `--gpus N` > 1 is asked for without WORLD_SIZE (bench.py then starts the N ranks itself), or
+    ("error", message) when --gpus and the launcher's WORLD_SIZE disagree (never a silent n_gpus: 1 line)."""
+    if gpus < 1:
+        return ("error", "--gpus must be >= 1, got %d" % gpus)
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        return ("spawn", gpus) if gpus > 1 else ("run", 1)
+    if int(ws) != gpus:
+        return ("error", "--gpus %d but the launcher started WORLD_SIZE=%s ranks" % (gpus, ws))
+    return ("run", gpus)
+
+
+def spawn_ranks(n, argv):
+    """Start `python -m torch.distributed.run --nproc-per-node n ... bench.py argv` as a CHILD process
+    (this process has not touched the GPU: no exec after GPU init) and return its exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the launcher and the rank bookkeeping without a GPU (gloo; CPU tests): every rank joins,
+    the max-over-ranks reduction runs, rank 0 prints the line's launcher fields."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True, "max_over_ranks": float(t.item())}), flush=True)
+    if world > 1:
         dist.destroy_process_group()
 
 
@@ -389,6 +466,7 @@ def main():
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU")
     ap.add_argument("--humans", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-steady", action="store_true", help="skip the steady_state window (100 + 2000 launches)")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--rng", choices=["mt19937", "philox"], default="mt19937",
                     help="reset / goal-change stream: mt19937 = the reference's numpy draws (default, the "
@@ -396,13 +474,23 @@ def main():
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2 = BASELINE metric (default); c3 / c4 / c5 are the SURVEY §8d side measurements "
                          "(c4: --steps / --warmup count PPO updates)")
+    ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    kind, val = launch_plan(args.gpus, os.environ)
+    if kind == "error":
+        print("bench.py: " + val, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if kind == "spawn":
+        sys.exit(spawn_ranks(val, sys.argv[1:]))
+    world = val
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
 
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -429,15 +517,19 @@ def main():
     else:
         engs = [CrowdNavEngine(make_config(E, N, rank * E, E * world, args.workload, args.rng), device)]
     eng = engs[0]
+    SW, SK = 100, 2000   # 100 warm-up steps, then >= 2,000 timed steps incl. all auto-resets
+    steady = not args.no_steady and (K < SK or W < SW)
     gen = torch.Generator(device=device)
     gen.manual_seed(rank)
-    acts = []
-    for e_ in engs:
+
+    def actions(T, e_):
         if args.workload == "c2":   # unicycle (dv, dtheta) ~ U[-0.1, 0.1]^2
-            a = torch.rand((K + W, e_.E, 2), generator=gen, device=device) * 0.2 - 0.1
+            a = torch.rand((T, e_.E, 2), generator=gen, device=device) * 0.2 - 0.1
         else:                       # holonomic (vx, vy) ~ N(0, 0.5^2), clipped by clip_action in the kernel
-            a = torch.randn((K + W, e_.E, 2), generator=gen, device=device) * 0.5
-        acts.append(a.contiguous())
+            a = torch.randn((T, e_.E, 2), generator=gen, device=device) * 0.5
+        return a.contiguous()
+
+    acts = [actions(K + W, e_) for e_ in engs]
     for e_ in engs:
         e_.reset()
     for s in range(W):
@@ -451,34 +543,51 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(device)
 
-    _lib.check(L.cn_profile(eng._h, 1, K))
-    barrier()
-    t0 = time.perf_counter()
-    for s in range(K):
-        for e_, a in zip(engs, acts):
-            e_.step(a[W + s])
-    barrier()
-    elapsed = time.perf_counter() - t0
-    a_ms, b_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
-    _lib.check(L.cn_profile_read(eng._h, ctypes.byref(a_ms), ctypes.byref(b_ms), ctypes.byref(n)))
-    _lib.check(L.cn_profile(eng._h, 0, 0))
-    done_frac = float(eng.done.float().mean().item())
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed_window(acts, first, count):
+        """count launches of every engine, timed between barriers (max over ranks); the step kernel's own
+        time from the two HIP events cn_step records around the window on its stream."""
+        r0 = reset_total(eng)
+        _lib.check(L.cn_profile(eng._h, 1, count))
+        barrier()
+        t0 = time.perf_counter()
+        for s in range(count):
+            for e_, a in zip(engs, acts):
+                e_.step(a[first + s])
+        barrier()
+        elapsed = time.perf_counter() - t0
+        a_ms, b_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        _lib.check(L.cn_profile_read(eng._h, ctypes.byref(a_ms), ctypes.byref(b_ms), ctypes.byref(n)))
+        _lib.check(L.cn_profile(eng._h, 0, 0))
+        resets = reset_total(eng) - r0
+        if dist is not None:
+            t = torch.tensor([elapsed, float(resets)], dtype=torch.float64, device=device)
+            dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+            elapsed, resets = float(t[0].item()), int(t[1].item())
+        return elapsed, a_ms.value / 1e3 / max(n.value, 1), resets
+
+    elapsed, kernel_s, resets = timed_window(acts, W, K)
+    done_frac = float(eng.done.float().mean().item())   # envs that ended an episode at the window's last step
+    st_win = None
+    if steady:
+        del acts
+        sacts = [actions(SW + SK, e_) for e_ in engs]
+        for s in range(SW):
+            for e_, a in zip(engs, sacts):
+                e_.step(a[s])
+        st_win = timed_window(sacts, SW, SK)
+        del sacts
 
     E_total = sum(e_.E for e_ in engs)
+    if args.workload == "c5":   # per group: its envs x B_step(its own N) (padding rows not counted)
+        hum = eng.env_humans.cpu().numpy()
+        bpl = int(sum(algorithmic_bytes_per_env_step(int(n)) for n in hum))
+    else:
+        bpl = algorithmic_bytes_per_env_step(eng.N) * eng.E
     if rank == 0:
         value = world * E_total * K / elapsed
-        kernel_s = a_ms.value / 1e3 / max(n.value, 1)   # c5: both group launches of a step
-        if args.workload == "c5":   # per group: its envs x B_step(its own N) (padding rows not counted)
-            hum = eng.env_humans.cpu().numpy()
-            bpl = int(sum(algorithmic_bytes_per_env_step(int(n)) for n in hum))
-        else:
-            bpl = algorithmic_bytes_per_env_step(eng.N) * eng.E
-        achieved = bpl / kernel_s / 1e9
-        pmc = load_pmc("cn_step_kernel", args.workload)
+        achieved = bpl / kernel_s / 1e9   # c5: kernel_s = both group launches of a step
+        pmc = load_pmc("cn_step_kernel", args.workload, window=(W, K))
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -499,22 +608,26 @@ def main():
                 "parallelism": "env-sharded x%d (no collective)" % world,
                 "rng": args.rng,
                 "step_kernel_ms": round(kernel_s * 1e3, 5),
+                "window": "launches %d..%d after cn_reset" % (W + 1, W + K),
+                "launches": [W, K],
+                "resets": resets,
+                "done_frac_last_step": round(done_frac, 5),
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 3),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6),
-                "traffic": round(pmc["traffic"]) if pmc else None,
-                "kernel": "cn_step_kernel",
-                "algorithmic_bytes_per_launch": bpl,
-                # what actually limits the kernel: dependent per-lane chains, not bandwidth
-                "limiter": "latency / issue (dependent f64 + f32 chains per lane; not HBM)",
-                "valu_issue_frac": round(pmc["valu_issue_frac"], 4) if pmc and pmc["valu_issue_frac"] else None,
-                "pmc_profile": ("profiles/pmc_%s.json" % pmc["tag"]) if pmc else None,
-            },
+            "roofline": roofline_obj(achieved, bpl, pmc),
         }
+        if st_win is not None:
+            s_el, s_ks, s_resets = st_win
+            s_pmc = load_pmc("cn_step_kernel", args.workload, window=(W + K + SW, SK))
+            line["steady_state"] = {
+                "value": round(world * E_total * SK / s_el, 1), "unit": "env-steps/s",
+                "warmup": SW, "steps": SK, "ms_per_step": round(s_el / SK * 1e3, 6),
+                "step_kernel_ms": round(s_ks * 1e3, 5),
+                "window": "launches %d..%d after cn_reset (SURVEY 8d: 100 warm-up + 2000 timed, incl. auto-resets)"
+                          % (W + K + SW + 1, W + K + SW + SK),
+                "launches": [W + K + SW, SK],
+                "resets": s_resets,
+                "roofline": roofline_obj(bpl / s_ks / 1e9, bpl, s_pmc),
+            }
         if not args.no_cpu_baseline and world == 1 and args.workload == "c2":
             line["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
         print(json.dumps(line), flush=True)
@@ -522,6 +635,26 @@ def main():
         e_.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def roofline_obj(achieved, bpl, pmc):
+    """The line's roofline object for the step kernel (SURVEY §8d B_step bytes per launch / its average
+    launch time); traffic / VALU issue from a hash-matched profile of the same window, else null."""
+    return {
+        "bound": "hbm",
+        "achieved": round(achieved, 3),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 6),
+        "traffic": round(pmc["traffic"]) if pmc and pmc.get("traffic") else None,
+        "kernel": "cn_step_kernel",
+        "algorithmic_bytes_per_launch": bpl,
+        # what actually limits the kernel (DESIGN §4): dependent per-lane chains, not bandwidth
+        "limiter": "latency / issue (dependent f64 + f32 chains per lane; not HBM)",
+        "valu_issue_frac": round(pmc["valu_issue_frac"], 4) if pmc and pmc.get("valu_issue_frac") else None,
+        "pmc_profile": ("profiles/pmc_%s.json" % pmc["tag"]) if pmc else None,
+        "pmc_avg_duration_us": round(pmc["avg_duration_ns"] / 1e3, 3) if pmc and pmc.get("avg_duration_ns") else None,
+    }
 
 
 if __name__ == "__main__":

@@ -533,15 +533,19 @@ __device__ __noinline__ bool robot_norm_zone_violation(double px, double py, dou
 
 __device__ inline float det2(float ax, float ay, float bx, float by) { return ax * by - ay * bx; }
 
-// a / b, IEEE-rounded, for the linear programs' quotients: |b| > RVO_EPSILON and modest finite operands.
-// This is the compiler's correctly rounded f32 division (v_div_scale, rcp, one reciprocal and two quotient
-// refinements by FMA, v_div_fmas, v_div_fixup) without the steps that are identities in that range:
-// v_div_scale only rescales a denormal divisor or an exponent gap of >= 96 (so VCC = 0 and v_div_fmas
-// is a plain FMA), and v_div_fixup only rewrites zero / inf / NaN operands and over/underflowed quotients.
-// Same bits, 8 instructions instead of 11, and no VCC chain serialising neighbouring divisions. The
-// callers ignore the quotient when |b| <= RVO_EPSILON (RVO2's parallel-line branch).
+// a / b, IEEE-rounded, for the linear programs' quotients: |b| > RVO_EPSILON (the callers ignore the
+// quotient when |b| <= RVO_EPSILON, RVO2's parallel-line branch) and |b| <= 2 (determinants of unit
+// direction vectors). This is the compiler's correctly rounded f32 division (v_div_scale, rcp, one
+// reciprocal and two quotient refinements by FMA, v_div_fmas, v_div_fixup) without the steps that are
+// identities on that domain: v_div_scale only rescales a denormal divisor or an exponent gap of >= 96
+// (so VCC = 0 and v_div_fmas is a plain FMA), and v_div_fixup only rewrites zero / inf / NaN operands and
+// over/underflowed quotients. The FMA residuals a - b*q are exact only while they stay above the denormal
+// range, i.e. for |a| >= ~2^-100: a numerator below 2^-96 (zero included) takes the full division instead
+// (a rarely taken branch). tools/fdiv_lp_check.hip compares this with `/` bit for bit over numerators of
+// every exponent (denormals included) and that divisor domain.
 __device__ __forceinline__ float fdiv_lp(float a, float b)
 {
+    if (__builtin_expect(__builtin_fabsf(a) < 0x1p-96f, 0)) return a / b;
     const float y0 = __builtin_amdgcn_rcpf(b);
     const float y1 = __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0);
     const float q0 = a * y1;

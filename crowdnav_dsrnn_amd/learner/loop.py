@@ -109,11 +109,18 @@ class RolloutTrainer:
         return ep_sum.clone(), ep_cnt.clone()
 
     def update(self):
-        t0 = time.perf_counter()
+        """One rollout + PPO update. rollout_s / update_s are GPU time between HIP events recorded on the
+        current stream (the side streams of the temporal GRU and the mixed engine fork from and join back to
+        it, so their work lies between the events); the update's one host sync (the losses) makes them
+        readable at the end."""
         c = self.config
         if c.training.use_linear_lr_decay:   # train.py:216-222, before the rollout of update j
             update_linear_schedule(self.agent.optimizer, self.update_index, self.num_updates, c.training.lr)
         self.update_index += 1
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if self.device.type == "cuda" else None
+        t0 = time.perf_counter()
+        if ev:
+            ev[0].record()
         ep_sum, ep_cnt = self.collect()
         r = self.rollouts
         with torch.no_grad():
@@ -123,11 +130,20 @@ class RolloutTrainer:
                                            r.masks[-1]).detach()
         r.compute_returns(next_value, c.ppo.use_gae, c.reward.gamma, c.ppo.gae_lambda,
                           c.training.use_proper_time_limits)
+        if ev:
+            ev[1].record()
         t1 = time.perf_counter()
         losses = self.agent.update(r)
         r.after_update()
-        t2 = time.perf_counter()
+        if ev:
+            ev[2].record()
         n = int(ep_cnt.item())
+        t2 = time.perf_counter()
+        if ev:
+            ev[2].synchronize()
+            rollout_s, update_s = ev[0].elapsed_time(ev[1]) / 1e3, ev[1].elapsed_time(ev[2]) / 1e3
+        else:
+            rollout_s, update_s = t1 - t0, t2 - t1
         return {"value_loss": losses[0], "action_loss": losses[1], "dist_entropy": losses[2],
                 "episodes": n, "mean_episode_return": float(ep_sum.item()) / max(n, 1),
-                "rollout_s": t1 - t0, "update_s": t2 - t1}
+                "rollout_s": rollout_s, "update_s": update_s, "host_s": t2 - t0}

@@ -12,9 +12,9 @@ ORCA keeps the reference's per-object simulator semantics (orca.py:85-115): the 
 every agent's ORCA radius (radius + 0.01 + safety_space) and max speed (own v_pref, others 1) -- is
 created at the first predict and only re-created when the number of agents changes; later calls only
 update positions and velocities. RVO2 works in float32 (positions, velocities, radii, the preferred
-velocity are cast at the boundary) and returns float32 velocities. Simulators of <= 10 agents (the
-engine's quad path); larger ones raise UnsupportedConfig (the step kernel's kd-tree path serves them
-inside cn_step).
+velocity are cast at the boundary) and returns float32 velocities. Simulators of <= 10 agents run on the
+engine's quad path (`cn_orca_predict`); 11 to 64 agents on the kd-tree path (`cn_orca_predict_kd`, RVO2's
+KdTree neighbour order with the persisted agents_ permutation); more than 64 raise UnsupportedConfig.
 """
 import collections
 import ctypes

@@ -39,3 +39,35 @@ def test_c5_mixed_config_round_robin():
     assert [c.num_envs for c in cfgs] == [int((eg == 0).sum()), int((eg == 1).sum())] == [3278, 4914]
     np.testing.assert_array_equal(eg, (np.arange(8192) % 5 >= 2).astype(np.int32))
     assert cfgs[1].side_preference == 1 and cfgs[1].circle_radius == 4 and cfgs[0].norm_zones == 1
+
+
+def test_launch_plan_never_reports_one_gpu_for_n():
+    """`bench.py --gpus N` without a launcher starts N ranks itself; under a launcher --gpus must equal
+    WORLD_SIZE (envs.py:120-139 builds the whole worker pool from one call)."""
+    assert bench.launch_plan(1, {}) == ("run", 1)
+    assert bench.launch_plan(8, {}) == ("spawn", 8)
+    assert bench.launch_plan(4, {"WORLD_SIZE": "4"}) == ("run", 4)
+    assert bench.launch_plan(8, {"WORLD_SIZE": "1"})[0] == "error"
+    assert bench.launch_plan(1, {"WORLD_SIZE": "2"})[0] == "error"
+    assert bench.launch_plan(0, {})[0] == "error"
+
+
+def test_single_command_two_rank_launch_gloo(tmp_path):
+    """`python bench.py --gpus 2` (no WORLD_SIZE) spawns two ranks through torch.distributed.run; with the
+    --dry-run hook each rank joins a gloo group and rank 0 prints n_gpus = 2 (no GPU touched)."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"), "--gpus", "2",
+                        "--steps", "3", "--warmup", "1", "--dry-run"], env=env, capture_output=True, text=True,
+                       timeout=240, cwd=str(tmp_path))
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["max_over_ranks"] == 2.0
+    # a mismatching launcher is refused (exit 2), not reported as a smaller run
+    env2 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    q = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"), "--gpus", "2",
+                        "--dry-run"], env=env2, capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
+    assert q.returncode == 2 and "WORLD_SIZE" in q.stderr
