@@ -396,7 +396,7 @@ def gen_dsrnn(outdir):
     import gym
 
     out = {}
-    for N in (5, 10):
+    for N in (5, 10, 25):   # N in {5, 10, 25} (25 = C3's spatial-edge width)
         E, T = 4, 8
         cfg = make_ref_config(N=N)
         cfg.training.cuda = False

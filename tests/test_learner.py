@@ -366,3 +366,91 @@ def test_rollout_hip_graph_matches_eager():
         for x, y in zip(a[:3], b[:3]):
             np.testing.assert_array_equal(x, y, err_msg="update %d" % u)
         assert a[3] == b[3]
+
+
+@pytest.mark.gpu
+def test_c4_shape_update_properties():
+    """C4's per-GPU shape: 4,096 envs x 10 humans, ORCA, holonomic, 128 steps, 5 epochs,
+    2 minibatches, HIP-graph rollouts. Properties at that size (no reference fixture covers it):
+    * graph == eager: three updates from the same start (the graph is captured at the second, replayed at
+      the third) give the same rollouts, losses and parameters bit for bit (deterministic actions);
+    * finite losses and parameters after every update;
+    * the Monitor's episode count of each rollout == the number of done flags it stored (masks == 0);
+    * the minibatch split of storage.py:228-234: torch.randperm(E) cut into num_mini_batch blocks of
+      E / num_mini_batch whole envs, every env exactly once, T * n rows per minibatch in (step, env) order,
+      the step-0 hidden states of exactly those envs."""
+    from crowdnav_dsrnn_amd.config import Config, clone_config
+    from crowdnav_dsrnn_amd.envs import CrowdNavVecEnv
+    from crowdnav_dsrnn_amd.learner.loop import RolloutTrainer
+
+    E4, N4, T4, MB = 4096, 10, 128, 2
+
+    def cfg():
+        c = clone_config(Config())
+        c.sim.human_num = N4
+        c.humans.policy = "orca"
+        c.action_space.kinematics = "holonomic"
+        c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+        c.training.num_processes = E4
+        c.ppo.num_steps = T4
+        c.ppo.epoch = 5
+        c.ppo.num_mini_batch = MB
+        c.training.lr = 4e-5
+        c.training.eps = 1e-5
+        c.training.max_grad_norm = 0.5
+        return c
+
+    def run(graphs, check_split=False):
+        c = cfg()
+        torch.manual_seed(11)
+        envs = CrowdNavVecEnv(c, E4, c.env.seed, "cuda:0", nenv=E4, phase="train")
+        pol = make_policy(N4, E=E4, T=T4, device="cuda:0")
+        agent = PPO(pol, c.ppo.clip_param, c.ppo.epoch, MB, c.ppo.value_loss_coef, c.ppo.entropy_coef,
+                    lr=c.training.lr, eps=c.training.eps, max_grad_norm=c.training.max_grad_norm)
+        tr = RolloutTrainer(c, envs, pol, agent, deterministic=True, graphs=graphs)
+        out = []
+        for u in range(3):
+            st = tr.update()
+            r = tr.rollouts
+            for k in ("value_loss", "action_loss", "dist_entropy"):
+                assert np.isfinite(st[k]), (u, k, st[k])
+            assert all(bool(torch.isfinite(p).all()) for p in pol.parameters()), u
+            dones = int((r.masks[1:] == 0).sum())
+            assert st["episodes"] == dones, (u, st["episodes"], dones)
+            out.append((r.actions.cpu().numpy().copy(), r.rewards.cpu().numpy().copy(),
+                        r.value_preds.cpu().numpy().copy(), st["episodes"], st["value_loss"], st["action_loss"]))
+        params = [p.detach().cpu().numpy().copy() for p in pol.parameters()]
+        if check_split:
+            r = tr.rollouts
+            adv = r.returns[:-1] - r.value_preds[:-1]
+            torch.manual_seed(123)
+            perm = torch.randperm(E4)
+            torch.manual_seed(123)
+            seen = []
+            h0 = r.recurrent_hidden_states["human_human_edge_rnn"][0]
+            n = E4 // MB
+            for b, mb in enumerate(r.recurrent_generator(adv, MB)):
+                ind = perm[b * n:(b + 1) * n].to(h0.device)
+                obs_b, hxs_b, act_b = mb[0], mb[1], mb[2]
+                assert act_b.shape == (T4 * n, 2)
+                assert obs_b["spatial_edges"].shape == (T4 * n, N4, 2)
+                torch.testing.assert_close(hxs_b["human_human_edge_rnn"], h0.index_select(0, ind), rtol=0, atol=0)
+                torch.testing.assert_close(act_b.view(T4, n, 2), r.actions.index_select(1, ind), rtol=0, atol=0)
+                seen.append(ind.cpu())
+            allv = torch.cat(seen)
+            assert len(seen) == MB and allv.numel() == E4 and torch.equal(torch.sort(allv).values, torch.arange(E4))
+        g = tr._graph is not None
+        envs.close()
+        del tr, agent, pol, envs
+        torch.cuda.empty_cache()
+        return out, params, g
+
+    eager, p_e, g0 = run(False)
+    graph, p_g, g1 = run(True, check_split=True)
+    assert not g0 and g1
+    for u, (a, b) in enumerate(zip(eager, graph)):
+        for x, y in zip(a[:3], b[:3]):
+            np.testing.assert_array_equal(x, y, err_msg="update %d" % u)
+        assert a[3:] == b[3:], u
+    for x, y in zip(p_e, p_g):
+        np.testing.assert_array_equal(x, y)

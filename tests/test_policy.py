@@ -73,7 +73,7 @@ def _check_eval(d, N, out):
     np.testing.assert_allclose(float(ent), float(d[p + "entropy"]), atol=ATOL, rtol=RTOL)
 
 
-@pytest.mark.parametrize("N", [5, 10])
+@pytest.mark.parametrize("N", [5, 10, 25])
 def test_state_dict_matches_reference_keys(dsrnn, N):
     pol = make_policy(N)
     sd = pol.state_dict()
@@ -92,7 +92,7 @@ def test_fused_kernel_is_mandatory():
     del pol
 
 
-@pytest.mark.parametrize("N", [5, 10])
+@pytest.mark.parametrize("N", [5, 10, 25])
 def test_policy_graph_cpu_with_fp32_input_layers(dsrnn, N, monkeypatch):
     """Everything but the fused kernel, on CPU: act + evaluate_actions (mid-sequence episode starts)."""
     from crowdnav_dsrnn_amd import ops
@@ -109,7 +109,7 @@ def test_policy_graph_cpu_with_fp32_input_layers(dsrnn, N, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [5, 10])
+@pytest.mark.parametrize("N", [5, 10, 25])
 def test_policy_act_gpu(dsrnn, N):
     _check_act(dsrnn, N, _run_act(dsrnn, N, "cuda:0"))
     _check_act(dsrnn, N, _run_act(dsrnn, N, "cuda:0", in_place=True))
@@ -118,7 +118,7 @@ def test_policy_act_gpu(dsrnn, N):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N", [5, 10])
+@pytest.mark.parametrize("N", [5, 10, 25])
 def test_policy_evaluate_actions_gpu(dsrnn, N):
     _check_eval(dsrnn, N, _run_eval(dsrnn, N, "cuda:0"))
 
