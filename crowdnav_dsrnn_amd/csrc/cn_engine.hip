@@ -80,6 +80,7 @@ __device__ unsigned long long cn_stamp_s[8192 * 16];   // spawn_env: start, seed
 struct StepPlan {
     int T;       // threads per workgroup (256)
     int H;       // human-lane stride (64: the humans of EPB envs sit on wave 0's lanes)
+    int NH;      // per-human stride of the ORCA scratch arrays (kd-tree path: EPB * N humans; quad path: H)
     int EPB;     // envs per workgroup
     int M;       // observed slots per human (ORCA lines upper bound)
     int A;       // agents per RVO2 simulator
@@ -116,6 +117,10 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.EPB = p.H / N < 16 ? p.H / N : 16;
     const int H = p.H;
     const int ML = p.M > 0 ? p.M : 1;
+    // the kd-tree path sizes its ORCA scratch for the workgroup's EPB * N humans (quads past them never
+    // touch it), so that three workgroups fit a CU's LDS
+    p.NH = p.kd ? p.EPB * N : H;
+    const int NH = p.NH;
     int o = 0;
     p.o_renv = o;  o = cn_align16(o + CN_RENV_F * p.EPB * 8);
     p.o_racts = o; o = cn_align16(o + 2 * p.EPB * 4);
@@ -127,24 +132,29 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_vis = o;   o = cn_align16(o + 3 * H * 4);          // visible mask, dummy mask, frozen max speed
     p.o_nv = o;    o = cn_align16(o + H * 16);             // post-move positions (x [H], y [H])
     p.o_eg = o;    o = cn_align16(o + H * 4);              // goal-reached / NaN flags
-    // ORCA, per human: sorted lines [H][M], projected lines [H][M], neighbour distances; kd: neighbour
-    // slots, KdTree agent order
-    p.o_lines = o; o = cn_align16(o + ML * H * 16);
-    p.o_proj = o;  o = cn_align16(o + ML * H * 16);
-    p.o_nd = o;    o = cn_align16(o + ML * H * 4);
-    p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * H : 0));
-    p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * H : 0));
-    // human velocity rectangles [8][H] (phases 1-2): over the quad path's projected-line / distance scratch,
-    // unused there since the linear programs keep their lines in registers; a region of their own otherwise
-    // + the human values human_post stages for the contiguous state / observation stores after phase 2 [7][H]
-    if (!p.kd && (p.o_ns - p.o_proj) >= 15 * H * 8) { p.o_hvr = p.o_proj; p.o_hst = p.o_proj + 8 * H * 8; }
+    // ORCA, per human: sorted lines [NH][M], projected lines [NH][M], neighbour distances (quad path); kd:
+    // neighbour slots [M][NH], KdTree agent order [A][NH]
+    p.o_lines = o; o = cn_align16(o + ML * NH * 16);
+    p.o_proj = o;  o = cn_align16(o + ML * NH * 16);
+    p.o_nd = o;    o = cn_align16(o + (p.kd ? 0 : ML * H * 4));
+    p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * NH : 0));
+    p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * NH : 0));
+    // human velocity rectangles [8][H] (phases 1-2) + the human values human_post stages for the contiguous
+    // state / observation stores after phase 2 [7][H]: over the quad path's projected-line / distance
+    // scratch, unused there since the linear programs keep their lines in registers. The kd-tree path keeps
+    // both in each human's own projected-line block instead (hvr_ref / hst_ref below): the rectangle is
+    // consumed at the start of phase 2, before that block holds the KdTree exchange, and the staged values
+    // are written after the human's linearProgram3, its last use of the block.
+    if (p.kd) { p.o_hvr = p.o_proj; p.o_hst = p.o_proj; }
+    else if ((p.o_ns - p.o_proj) >= 15 * H * 8) { p.o_hvr = p.o_proj; p.o_hst = p.o_proj + 8 * H * 8; }
     else { p.o_hvr = o; p.o_hst = o + 8 * H * 8; o = cn_align16(o + 15 * H * 8); }
     // quad path: the workgroup's linearProgram3 sub-problems (lp3_tasks): per human fail | n << 8, results
     // [H][12] (phase 2 only: under the RNG regions)
     p.o_l3b = o;   o = cn_align16(o + (p.kd ? 0 : H * 4));
     p.o_l3r = o;   o = cn_align16(o + (p.kd ? 0 : H * 12 * 8));
     p.o_l3k = o;   o = cn_align16(o + (p.kd ? 0 : H * 12));
-    p.rng_waves = 4;
+    // one RNG wave per env of the workgroup, at most 4 (kd-tree path: EPB = 2 or 5 envs)
+    p.rng_waves = p.EPB < 4 ? p.EPB : 4;
     // the DiscGrid region only where it costs no LDS (the kd-tree path's ORCA scratch is larger than the
     // RNG regions it hosts); the quad path keeps its 3 workgroups per CU
     p.rng_stride = p.o_lines + p.rng_waves * (CN_PEND_LDS + CN_GRID_LDS) <= o ? CN_PEND_LDS + CN_GRID_LDS : CN_PEND_LDS;
@@ -2224,7 +2234,7 @@ __device__ inline float bbox_dist(float x, float y, float mnx, float mxx, float 
 // compile-time constant and costs no registers
 // DEVSEQ: graph mode (StepArgs::devseq), a variant of its own so the default launches carry none of it
 template <bool KD, bool PHX, bool MIX, bool DEVSEQ = false>
-__global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g, cn_config c)
+__global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_config c)
 {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const OutView ov = MIX ? g.ov : OutView{nullptr, c.human_num};
@@ -2305,6 +2315,14 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     sl.ns = (uint8_t *)(smem + P.o_ns);
     sl.perm = (uint8_t *)(smem + P.o_perm);
     const cn_state_ptrs &S = g.s;
+    // human hh's velocity-rectangle corner k (x0..x3, y0..y3) and human_post's staged value f: [8][H] / [7][H]
+    // arrays on the quad path, the human's own projected-line block on the kd-tree path (StepPlan)
+    auto hvr_ref = [&](int hh, int k) -> double & {
+        return KD ? ((double *)(sl.proj + hh * M))[k] : sl.hvr[k * 64 + hh];
+    };
+    auto hst_ref = [&](int hh, int f) -> double & {
+        return KD ? ((double *)(sl.proj + hh * M))[f] : sl.hst[f * 64 + hh];
+    };
 
     const int tid = threadIdx.x;
     // XCD-aware env placement: workgroup i runs on XCD i % 8 (round-robin dispatch; for speed only), so
@@ -2409,7 +2427,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         sl.cd[hh] = dsqrt(rdx * rdx + rdy * rdy) - rad - RF(sl, R_RAD, elh, EPB);
         double hcx[4], hcy[4];
         vel_rect(px, py, vx0, vy0, rad, false, hcx, hcy);
-        for (int k = 0; k < 4; ++k) { sl.hvr[k * 64 + hh] = hcx[k]; sl.hvr[(4 + k) * 64 + hh] = hcy[k]; }
+        for (int k = 0; k < 4; ++k) { hvr_ref(hh, k) = hcx[k]; hvr_ref(hh, 4 + k) = hcy[k]; }
         // (the path-violation test of this rectangle against the robot's runs in human_post, phase 2: the
         // robot's rectangle is computed beside this one, on wave 3)
         uint32_t f = 0u;
@@ -2640,7 +2658,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         double rcx[4], rcy[4], hcx[4], hcy[4];
         for (int k = 0; k < 4; ++k) {
             rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh];
-            hcx[k] = sl.hvr[k * 64 + hh]; hcy[k] = sl.hvr[(4 + k) * 64 + hh];
+            hcx[k] = hvr_ref(hh, k); hcy[k] = hvr_ref(hh, 4 + k);
         }
         return quads_intersect_q(rcx, rcy, hcx, hcy, s4);
     };
@@ -2649,7 +2667,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         double rcx[4], rcy[4], hcx[4], hcy[4];
         for (int k = 0; k < 4; ++k) {
             rcx[k] = sl.rvr[k * EPB + elh]; rcy[k] = sl.rvr[(4 + k) * EPB + elh];
-            hcx[k] = sl.hvr[k * 64 + hh]; hcy[k] = sl.hvr[(4 + k) * 64 + hh];
+            hcx[k] = hvr_ref(hh, k); hcy[k] = hvr_ref(hh, 4 + k);
         }
         return quads_intersect(rcx, rcy, hcx, hcy);
     };
@@ -2687,9 +2705,9 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
         // staged in LDS: the state / observation stores go out after phase 2 from consecutive lanes (one
         // lane per quad here would split every 128-B line of a field over several waves' partial writes:
         // +4 MB of HBM writes per C2 launch, measured)
-        sl.hst[0 * 64 + hh] = nvx; sl.hst[1 * 64 + hh] = nvy;
-        sl.hst[2 * 64 + hh] = bpx; sl.hst[3 * 64 + hh] = bpy; sl.hst[4 * 64 + hh] = bvx; sl.hst[5 * 64 + hh] = bvy;
-        sl.hst[6 * 64 + hh] = br;
+        hst_ref(hh, 0) = nvx; hst_ref(hh, 1) = nvy;
+        hst_ref(hh, 2) = bpx; hst_ref(hh, 3) = bpy; hst_ref(hh, 4) = bvx; hst_ref(hh, 5) = bvy;
+        hst_ref(hh, 6) = br;
         uint32_t f = vr ? LF_VR : 0u;
         if (np_norm2(HF(sl, H_GX, hh) - npx, HF(sl, H_GY, hh) - npy) < HF(sl, H_R, hh)) f |= LF_ENDGOAL;
         if (!(npx == npx) || !(npy == npy)) f |= 0x80000000u;
@@ -2729,6 +2747,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                 const double speed = np_norm2(gdx, gdy);
                 if (speed > 1.0) { gdx = ddiv(gdx, speed); gdy = ddiv(gdy, speed); }
                 float4 *Lb = sl.lines + h * M, *Pb = sl.proj + h * M;
+                bool vr_kd = false;   // kd-tree path: path violation, tested before Pb is reused
                 int cnt = 0;
                 uint32_t inm = 0;
                 if constexpr (!KD) {
@@ -2742,9 +2761,13 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                     // (1) the quad loads the persisted KdTree order and fills, in that order, the agents'
                     //     positions (XYP[q] = agent perm[q]: self = 0, slot k = k + 1; kept in the projected-
                     //     lines space, unused until linearProgram3) and each slot's distSq
-                    const int HS = sl.T;   // LDS stride of the per-human slot / KdTree order arrays
-                    float *D = sl.nd + h * M;
-                    float2 *XYP = (float2 *)Pb;
+                    // (0) the path-violation test reads this human's velocity rectangle from Pb, which the
+                    //     KdTree exchange reuses below
+                    if (hq) vr_kd = path_vr_q(h, sq);   // the whole quad
+                    wsync();
+                    const int HS = P.NH;   // LDS stride of the per-human slot / KdTree order arrays
+                    float2 *XYP = (float2 *)Pb;          // [A] (x, y) in KdTree order, then the exchange space
+                    float *D = (float *)Pb + 2 * A;      // [M] distSq of each slot (beside XYP in Pb)
                     uint8_t *perm = sl.perm, *tpos = sl.ns;
                     const bool frz = (sl.rflag[elq] & CN_FLAG_ORCA_FROZEN) != 0;
                     const int gq = (e0 + elq) * N + iq;
@@ -2789,9 +2812,10 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                             const int hw = wbase + grp;
                             const int elw = hw / N, iw = hw - elw * N;
                             const int gw = (e0 + elw) * N + iw;
-                            const float *Dw = sl.nd + hw * M;
                             int4 *stk = (int4 *)(sl.lines + hw * M);
-                            float *xch = (float *)(sl.proj + hw * M);   // 2 x (A / 2) entries of (x, y, a)
+                            // exchange: (x, y) of 2 x (A / 2) entries in Pb, their agent ids in perm (read once
+                            // above); a slot's in-range test is bit (agent - 1) of the quad's inm
+                            float *xch = (float *)(sl.proj + hw * M);
                             const float SX = (float)HF(sl, H_PX, hw), SY = (float)HF(sl, H_PY, hw);
                             float px[8], py[8];
                             int pa[8], qq[8];
@@ -2841,7 +2865,7 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                                 if (e1 - b0 <= 10) {   // leaf (RVO_MAX_LEAF_SIZE): insert in position order
 #pragma unroll
                                     for (int u = 0; u < 8; ++u)
-                                        pr[u] = qq[u] >= b0 && qq[u] < e1 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
+                                        pr[u] = qq[u] >= b0 && qq[u] < e1 && pa[u] != 0 && ((inm >> (pa[u] - 1)) & 1u);
                                     const uint32_t bits = gmask(pr);
 #pragma unroll
                                     for (int u = 0; u < 8; ++u)
@@ -2858,12 +2882,12 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                                     // visited right first: positions [e1-10, e1) in order, then e1-11 down to b0
 #pragma unroll
                                     for (int u = 0; u < 8; ++u)
-                                        pr[u] = qq[u] >= e1 - 10 && qq[u] < e1 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
+                                        pr[u] = qq[u] >= e1 - 10 && qq[u] < e1 && pa[u] != 0 && ((inm >> (pa[u] - 1)) & 1u);
                                     const uint32_t b1 = gmask(pr);
                                     bool p2[8];
 #pragma unroll
                                     for (int u = 0; u < 8; ++u)
-                                        p2[u] = qq[u] >= b0 && qq[u] < e1 - 10 && pa[u] != 0 && Dw[pa[u] - 1] < rangeSq;
+                                        p2[u] = qq[u] >= b0 && qq[u] < e1 - 10 && pa[u] != 0 && ((inm >> (pa[u] - 1)) & 1u);
                                     const uint32_t b2 = gmask(p2);
 #pragma unroll
                                     for (int u = 0; u < 8; ++u) {
@@ -2899,16 +2923,17 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                                         slot[u] = pL[u] ? __popc(Lm & ((1u << qq[u]) - 1u))
                                                         : nsw + __popc(Rm >> qq[u] >> 1);
                                         if (pL[u] || pR[u]) {
-                                            float *o = xch + 3 * slot[u];
-                                            o[0] = px[u]; o[1] = py[u]; o[2] = __int_as_float(pa[u]);
+                                            float *o = xch + 2 * slot[u];
+                                            o[0] = px[u]; o[1] = py[u]; perm[slot[u] * HS + hw] = (uint8_t)pa[u];
                                         }
                                     }
                                     wsync();
 #pragma unroll
                                     for (int u = 0; u < 8; ++u) {
                                         if (pL[u] || pR[u]) {
-                                            const float *o = xch + 3 * (pL[u] ? slot[u] + nsw : slot[u] - nsw);
-                                            px[u] = o[0]; py[u] = o[1]; pa[u] = __float_as_int(o[2]);
+                                            const int src = pL[u] ? slot[u] + nsw : slot[u] - nsw;
+                                            const float *o = xch + 2 * src;
+                                            px[u] = o[0]; py[u] = o[1]; pa[u] = perm[src * HS + hw];
                                         }
                                     }
                                     wsync();
@@ -3019,8 +3044,8 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
                     STAMP_A(8);
                     if (fail_at < cnt) lp3_q(Lb, Pb, cnt, fail_at, vmq, sq, rx, ry);
                     STAMP_A(9);
-                    const bool vr = path_vr_q(h, sq);   // the whole quad
-                    if (sq == 0) human_post(h, (double)rx, (double)ry, vr);
+                    wsync();   // the quad's last reads of Pb (linearProgram3) before human_post stages into it
+                    if (sq == 0) human_post(h, (double)rx, (double)ry, vr_kd);
                 }
             }
         } else if (hl) {
@@ -3069,10 +3094,10 @@ __global__ void __launch_bounds__(CN_BLK, KD ? 2 : 3) cn_step_kernel(StepArgs g,
     //      and observation stores and RNG needs (env lanes) ---------------------------------------------
     if (hl) {
         S.h_px[gh] = sl.npx[tid]; S.h_py[gh] = sl.npy[tid];
-        S.h_vx[gh] = sl.hst[0 * 64 + tid]; S.h_vy[gh] = sl.hst[1 * 64 + tid];
-        const double bpx = sl.hst[2 * 64 + tid], bpy = sl.hst[3 * 64 + tid];
-        S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = sl.hst[4 * 64 + tid]; S.b_vy[gh] = sl.hst[5 * 64 + tid];
-        S.b_r[gh] = sl.hst[6 * 64 + tid];
+        S.h_vx[gh] = hst_ref(tid, 0); S.h_vy[gh] = hst_ref(tid, 1);
+        const double bpx = hst_ref(tid, 2), bpy = hst_ref(tid, 3);
+        S.b_px[gh] = bpx; S.b_py[gh] = bpy; S.b_vx[gh] = hst_ref(tid, 4); S.b_vy[gh] = hst_ref(tid, 5);
+        S.b_r[gh] = hst_ref(tid, 6);
         const int64_t oh = orow(ov, e0 + el) * ov.NS + i;
         g.spatial[oh * 2] = (float)(bpx - RF(sl, R_NX, el, EPB));
         g.spatial[oh * 2 + 1] = (float)(bpy - RF(sl, R_NY, el, EPB));

@@ -68,6 +68,7 @@ class CrowdNavEngine:
         self.info = torch.zeros((E, abi.INFO_K), dtype=torch.float32, device=dev)
         self.ep_return = torch.zeros((E,), dtype=torch.float64, device=dev)
         self.ep_len = torch.zeros((E,), dtype=torch.int32, device=dev)
+        self._step_args = None   # cached output pointers of step() (the buffers above are never reallocated)
 
     @classmethod
     def mixed(cls, cfgs, env_group, device=None):
@@ -98,12 +99,20 @@ class CrowdNavEngine:
             actions = actions.to(device=self.device, dtype=t.float32).contiguous()
         if actions.numel() != self.E * 2:
             raise ValueError("actions must have E*2 = %d elements, got %d" % (self.E * 2, actions.numel()))
-        with t.cuda.device(self.device):
-            _lib.check(_lib.lib().cn_step(
-                self._h, self._stream(), actions.data_ptr(), self.robot_node.data_ptr(),
-                self.temporal_edges.data_ptr(), self.spatial_edges.data_ptr(), self.reward.data_ptr(),
-                self.done.data_ptr(), self.event.data_ptr(), self.info.data_ptr(), self.ep_return.data_ptr(),
-                self.ep_len.data_ptr()))
+        # host cost per call matters when a short window starts on an idle GPU: the output pointers and the
+        # bound C function are cached, and the device guard is entered only when another device is current
+        if self._step_args is None:
+            self._step_fn = _lib.lib().cn_step
+            self._step_args = (self.robot_node.data_ptr(), self.temporal_edges.data_ptr(),
+                               self.spatial_edges.data_ptr(), self.reward.data_ptr(), self.done.data_ptr(),
+                               self.event.data_ptr(), self.info.data_ptr(), self.ep_return.data_ptr(),
+                               self.ep_len.data_ptr())
+        if t.cuda.current_device() == self.device.index:
+            rc = self._step_fn(self._h, t.cuda.current_stream().cuda_stream, actions.data_ptr(), *self._step_args)
+        else:
+            with t.cuda.device(self.device):
+                rc = self._step_fn(self._h, t.cuda.current_stream().cuda_stream, actions.data_ptr(), *self._step_args)
+        _lib.check(rc)
         return self.obs(), self.reward, self.done, self.event, self.info, self.ep_return, self.ep_len
 
     def set_graph_mode(self, on=True):
