@@ -137,8 +137,8 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     p.o_lines = o; o = cn_align16(o + ML * NH * 16);
     p.o_proj = o;  o = cn_align16(o + ML * NH * 16);
     p.o_nd = o;    o = cn_align16(o + (p.kd ? 0 : ML * H * 4));
-    p.o_ns = o;    o = cn_align16(o + (p.kd ? ML * NH : 0));
-    p.o_perm = o;  o = cn_align16(o + (p.kd ? p.A * NH : 0));
+    p.o_ns = o;    o = cn_align16(o + (p.kd ? (ML + 1) * NH : 0));      // + a dummy row (the KdTree walk)
+    p.o_perm = o;  o = cn_align16(o + (p.kd ? (p.A + 1) * NH : 0));     // + a dummy row
     // human velocity rectangles [8][H] (phases 1-2) + the human values human_post stages for the contiguous
     // state / observation stores after phase 2 [7][H]: over the quad path's projected-line / distance
     // scratch, unused there since the linear programs keep their lines in registers. The kd-tree path keeps
@@ -246,6 +246,28 @@ __device__ inline bool in_fov(double fx, double fy, double px1, double py1, doub
     if (d > cth + 1e-12) return true;
     if (d < cth - 1e-12) return false;
     return acos_within(d, fov);
+}
+
+// in_fov decided without square roots or divisions where that is exact (FOV < 2 pi; the pair loops of
+// phase 1 and the robot's belief test): d = (f . v) / |v| against thresholds 4e-12 either side of cth, as
+// sign tests of dp = f . v and of dp^2 - t^2 |v|^2 (d > t <=> dp > t |v|). These are within a few 1e-16 of
+// the exact values, and the reference's d (correctly rounded norm, divisions and dot product, in_fov)
+// within a few 1e-16 of the exact d too, so outside the +-4e-12 band both sides of cth are decided alike;
+// inside it (and for |v|^2 near under/overflow or zero: coincident agents) in_fov itself runs.
+__device__ inline bool in_fov_fast(double fx, double fy, double px1, double py1, double px2, double py2, double fov,
+                                   double cth)
+{
+    const double dx = px2 - px1, dy = py2 - py1;
+    const double n2 = __fma_rn(dy, dy, dx * dx);
+    if (n2 > 1e-200 && n2 < 1e200) {
+        const double dp = __fma_rn(fy, dy, fx * dx), dp2 = dp * dp;
+        const double hi = cth + 4e-12, lo = cth - 4e-12;
+        const bool above = hi >= 0.0 ? (dp > 0.0 && dp2 > hi * hi * n2) : (dp >= 0.0 || dp2 < hi * hi * n2);
+        if (above) return true;
+        const bool below = lo > 0.0 ? (dp <= 0.0 || dp2 < lo * lo * n2) : (dp < 0.0 && dp2 > lo * lo * n2);
+        if (below) return false;
+    }
+    return in_fov(fx, fy, px1, py1, px2, py2, fov, cth);
 }
 
 // the robot's FOV test of a freshly spawned human (generate_ob(reset=True)), out of line: inlined into the
@@ -2535,13 +2557,13 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             const int k = __ffs(um) - 1;
             const int j = eb + (k < i ? k : k + 1);
             dir();
-            if (in_fov(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov, g.cth_h)) vis |= 1u << k;
+            if (in_fov_fast(fx, fy, px, py, HF(sl, H_PX, j), HF(sl, H_PY, j), c.human_fov, g.cth_h)) vis |= 1u << k;
         }
         if (c.robot_visible) {
             int v = full ? vis360(hfin, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB)) : -1;
             if (v < 0) {
                 dir();
-                v = in_fov(fx, fy, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB), c.human_fov, g.cth_h) ? 1 : 0;
+                v = in_fov_fast(fx, fy, px, py, RF(sl, R_PX, el, EPB), RF(sl, R_PY, el, EPB), c.human_fov, g.cth_h) ? 1 : 0;
             }
             if (v) vis |= 1u << (N - 1);
         }
@@ -2688,7 +2710,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             double fx, fy;
             if (holo) fov_dir32(atan2f(rvy, rvx), fx, fy);
             else fov_dir32(rth, fx, fy);
-            rv = in_fov(fx, fy, rnx, rny, npx, npy, c.robot_fov, g.cth_r) ? 1 : 0;
+            rv = in_fov_fast(fx, fy, rnx, rny, npx, npy, c.robot_fov, g.cth_r) ? 1 : 0;
         }
         double bpx, bpy, bvx, bvy, br;
         if (rv) {
@@ -2798,15 +2820,19 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                     //     nothing: the in-range agents' visiting order tpos is the order
                     //     Agent::insertAgentNeighbor sees. The explicit stack (<= A - 9 entries) lives in the
                     //     sorted-lines space, written only after the walk.
+                    //     The body is predicated rather than branched per element: every element's LDS write goes
+                    //     to its slot or to a dummy slot of the human (tpos row M, perm row A, the exchange entry
+                    //     XD past the distances), every read comes from a valid address and is selected, and the
+                    //     group masks are quad ORs of per-lane bit sets (lane sub holds positions sub + 4u).
                     {
                         const int lane = tid & 63, grp = lane >> 2, sub = lane & 3;
                         const int wbase = (tid >> 6) * 16;
+                        const uint32_t sbit = 1u << sub;
                         auto gmask = [&](const bool (&pr)[8]) -> uint32_t {
                             uint32_t m = 0;
 #pragma unroll
-                            for (int u = 0; u < 8; ++u)
-                                m |= (uint32_t)((__ballot(pr[u]) >> (4 * grp)) & 0xfull) << (4 * u);
-                            return m;
+                            for (int u = 0; u < 8; ++u) m |= pr[u] ? (sbit << (4 * u)) : 0u;
+                            return (uint32_t)quad_or((int)m);
                         };
                         if (wbase + grp < nh) {   // 16 humans per wave, 4 lanes each, all at once
                             const int hw = wbase + grp;
@@ -2815,26 +2841,31 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                             int4 *stk = (int4 *)(sl.lines + hw * M);
                             // exchange: (x, y) of 2 x (A / 2) entries in Pb, their agent ids in perm (read once
                             // above); a slot's in-range test is bit (agent - 1) of the quad's inm
-                            float *xch = (float *)(sl.proj + hw * M);
+                            float2 *xch = (float2 *)(sl.proj + hw * M);
+                            const int XD = (2 * A + M + 1) / 2;   // dummy exchange entry (floats [2A + M, 4M) are free)
+                            uint8_t *permw = perm + hw, *tposw = tpos + hw;
                             const float SX = (float)HF(sl, H_PX, hw), SY = (float)HF(sl, H_PY, hw);
                             float px[8], py[8];
-                            int pa[8], qq[8];
+                            int pa[8];
+                            bool inr[8];   // element u is an agent within range (bit pa - 1 of inm)
 #pragma unroll
                             for (int u = 0; u < 8; ++u) {
-                                qq[u] = sub + 4 * u;
-                                const bool v = qq[u] < A;
-                                const float2 t = v ? ((const float2 *)xch)[qq[u]] : make_float2(0.0f, 0.0f);
-                                px[u] = t.x; py[u] = t.y;
-                                pa[u] = v ? perm[qq[u] * HS + hw] : 0;
+                                const int q = sub + 4 * u;
+                                const bool v = q < A;
+                                const float2 t = xch[v ? q : XD];
+                                px[u] = v ? t.x : 0.0f; py[u] = v ? t.y : 0.0f;
+                                const int a = permw[(v ? q : A) * HS];
+                                pa[u] = v ? a : 0;
+                                inr[u] = pa[u] != 0 && ((inm >> ((pa[u] - 1) & 31)) & 1u);
                             }
                             auto red = [&](int b0, int e1, float &mnx, float &mxx, float &mny, float &mxy) {
                                 float a0 = INFINITY, a1 = -INFINITY, c0 = INFINITY, c1 = -INFINITY;
 #pragma unroll
                                 for (int u = 0; u < 8; ++u) {
-                                    if (qq[u] >= b0 && qq[u] < e1) {
-                                        a1 = a1 < px[u] ? px[u] : a1; a0 = px[u] < a0 ? px[u] : a0;
-                                        c1 = c1 < py[u] ? py[u] : c1; c0 = py[u] < c0 ? py[u] : c0;
-                                    }
+                                    const int q = sub + 4 * u;
+                                    const bool in = q >= b0 && q < e1;
+                                    a1 = in && a1 < px[u] ? px[u] : a1; a0 = in && px[u] < a0 ? px[u] : a0;
+                                    c1 = in && c1 < py[u] ? py[u] : c1; c0 = in && py[u] < c0 ? py[u] : c0;
                                 }
                                 mnx = quad_min(a0); mxx = quad_max(a1); mny = quad_min(c0); mxy = quad_max(c1);
                             };
@@ -2861,80 +2892,71 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
 #endif
                                 const int4 en = stk[--sp];
                                 const int b0 = en.x, e1 = en.y;
-                                bool pr[8];
-                                if (e1 - b0 <= 10) {   // leaf (RVO_MAX_LEAF_SIZE): insert in position order
-#pragma unroll
-                                    for (int u = 0; u < 8; ++u)
-                                        pr[u] = qq[u] >= b0 && qq[u] < e1 && pa[u] != 0 && ((inm >> (pa[u] - 1)) & 1u);
-                                    const uint32_t bits = gmask(pr);
-#pragma unroll
-                                    for (int u = 0; u < 8; ++u)
-                                        if (pr[u])
-                                            tpos[(pa[u] - 1) * HS + hw] =
-                                                (uint8_t)(tc + __popc(bits & ((1u << qq[u]) - 1u)));
-                                    tc += __popc(bits);
-                                    continue;
-                                }
-                                if (en.z & 2) {
-                                    // coincident points (e.g. the dummies of unseen humans, all at (7, 7)): no
-                                    // split separates them, so each level peels its first element into a
-                                    // one-agent leaf, nothing moves, and the equal-distance children are
-                                    // visited right first: positions [e1-10, e1) in order, then e1-11 down to b0
-#pragma unroll
-                                    for (int u = 0; u < 8; ++u)
-                                        pr[u] = qq[u] >= e1 - 10 && qq[u] < e1 && pa[u] != 0 && ((inm >> (pa[u] - 1)) & 1u);
-                                    const uint32_t b1 = gmask(pr);
-                                    bool p2[8];
-#pragma unroll
-                                    for (int u = 0; u < 8; ++u)
-                                        p2[u] = qq[u] >= b0 && qq[u] < e1 - 10 && pa[u] != 0 && ((inm >> (pa[u] - 1)) & 1u);
-                                    const uint32_t b2 = gmask(p2);
-#pragma unroll
-                                    for (int u = 0; u < 8; ++u) {
-                                        if (pr[u])
-                                            tpos[(pa[u] - 1) * HS + hw] = (uint8_t)(tc + __popc(b1 & ((1u << qq[u]) - 1u)));
-                                        if (p2[u])
-                                            tpos[(pa[u] - 1) * HS + hw] =
-                                                (uint8_t)(tc + __popc(b1) + __popc(b2 >> qq[u] >> 1));
-                                    }
-                                    tc += __popc(b1) + __popc(b2);
-                                    continue;
-                                }
-                                const float split = __int_as_float(en.w);
-                                bool lt[8], pL[8], pR[8];
+                                const bool leaf = e1 - b0 <= 10;           // RVO_MAX_LEAF_SIZE
+                                const bool deg = !leaf && (en.z & 2) != 0;
+                                // insertions of a leaf (positions [b0, e1) in order) or of a node whose points all
+                                // coincide (e.g. the dummies of unseen humans, all at (7, 7)): no split separates
+                                // them, so each level peels its first element into a one-agent leaf, nothing moves,
+                                // and the equal-distance children are visited right first: positions [e1-10, e1) in
+                                // order (set 1), then e1-11 down to b0 (set 2). Internal nodes insert nothing.
+                                const int lo1 = leaf ? b0 : (deg ? e1 - 10 : e1), hi2 = deg ? e1 - 10 : b0;
+                                bool s1[8], s2[8];
 #pragma unroll
                                 for (int u = 0; u < 8; ++u) {
+                                    const int q = sub + 4 * u;
+                                    s1[u] = q >= lo1 && q < e1 && inr[u];
+                                    s2[u] = q >= b0 && q < hi2 && inr[u];
+                                }
+                                const uint32_t b1 = gmask(s1), b2 = gmask(s2);
+#pragma unroll
+                                for (int u = 0; u < 8; ++u) {
+                                    const int q = sub + 4 * u;
+                                    const int r1 = tc + __popc(b1 & ((1u << q) - 1u));
+                                    const int r2 = tc + __popc(b1) + __popc(b2 >> q >> 1);
+                                    const bool w = s1[u] || s2[u];
+                                    tposw[(w ? pa[u] - 1 : M) * HS] = (uint8_t)(s1[u] ? r1 : r2);
+                                }
+                                tc += __popc(b1) + __popc(b2);
+                                if (leaf || deg) continue;
+                                const float split = __int_as_float(en.w);
+                                bool lt[8], pr[8], pL[8], pR[8];
+#pragma unroll
+                                for (int u = 0; u < 8; ++u) {
+                                    const int q = sub + 4 * u;
                                     lt[u] = ((en.z & 1) ? px[u] : py[u]) < split;
-                                    pr[u] = qq[u] >= b0 && qq[u] < e1 && lt[u];
+                                    pr[u] = q >= b0 && q < e1 && lt[u];
                                 }
                                 const int mid = b0 + __popc(gmask(pr));
 #pragma unroll
                                 for (int u = 0; u < 8; ++u) {
-                                    const bool in = qq[u] >= b0 && qq[u] < e1;
-                                    pL[u] = in && qq[u] < mid && !lt[u];
-                                    pR[u] = in && qq[u] >= mid && lt[u];
+                                    const int q = sub + 4 * u;
+                                    const bool in = q >= b0 && q < e1;
+                                    pL[u] = in && q < mid && !lt[u];
+                                    pR[u] = in && q >= mid && lt[u];
                                 }
                                 const uint32_t Lm = gmask(pL), Rm = gmask(pR);
-                                if (Lm) {
+                                if (Lm) {   // Hoare's swaps: the i-th misplaced left element with the i-th right one
                                     const int nsw = __popc(Lm);
-                                    int slot[8];
+                                    int src[8];
 #pragma unroll
                                     for (int u = 0; u < 8; ++u) {
-                                        slot[u] = pL[u] ? __popc(Lm & ((1u << qq[u]) - 1u))
-                                                        : nsw + __popc(Rm >> qq[u] >> 1);
-                                        if (pL[u] || pR[u]) {
-                                            float *o = xch + 2 * slot[u];
-                                            o[0] = px[u]; o[1] = py[u]; perm[slot[u] * HS + hw] = (uint8_t)pa[u];
-                                        }
+                                        const int q = sub + 4 * u;
+                                        const bool mv = pL[u] || pR[u];
+                                        const int slot = pL[u] ? __popc(Lm & ((1u << q) - 1u)) : nsw + __popc(Rm >> q >> 1);
+                                        const int ws = mv ? slot : XD;
+                                        xch[ws] = make_float2(px[u], py[u]);
+                                        permw[(mv ? slot : A) * HS] = (uint8_t)pa[u];
+                                        src[u] = mv ? (pL[u] ? slot + nsw : slot - nsw) : -1;
                                     }
                                     wsync();
 #pragma unroll
                                     for (int u = 0; u < 8; ++u) {
-                                        if (pL[u] || pR[u]) {
-                                            const int src = pL[u] ? slot[u] + nsw : slot[u] - nsw;
-                                            const float *o = xch + 2 * src;
-                                            px[u] = o[0]; py[u] = o[1]; pa[u] = perm[src * HS + hw];
-                                        }
+                                        const bool mv = src[u] >= 0;
+                                        const float2 t = xch[mv ? src[u] : XD];
+                                        const int a = permw[(mv ? src[u] : A) * HS];
+                                        px[u] = mv ? t.x : px[u]; py[u] = mv ? t.y : py[u];
+                                        pa[u] = mv ? a : pa[u];
+                                        inr[u] = pa[u] != 0 && ((inm >> ((pa[u] - 1) & 31)) & 1u);
                                     }
                                     wsync();
                                 }
@@ -2945,16 +2967,17 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                                 const int4 cl = entry(b0, left, l0, l1, l2, l3), cr = entry(left, e1, r0, r1, r2, r3);
                                 const float dl = bbox_dist(SX, SY, l0, l1, l2, l3);
                                 const float dr = bbox_dist(SX, SY, r0, r1, r2, r3);
-                                if (sub == 0) {
-                                    if (dl < dr) { stk[sp] = cr; stk[sp + 1] = cl; }   // left visited first
-                                    else { stk[sp] = cl; stk[sp + 1] = cr; }
-                                }
+                                // (all 4 lanes store the same entries) left visited first when strictly closer
+                                stk[sp] = dl < dr ? cr : cl;
+                                stk[sp + 1] = dl < dr ? cl : cr;
                                 sp += 2;
                                 wsync();
                             }
 #pragma unroll
-                            for (int u = 0; u < 8; ++u)
-                                if (qq[u] < A) S.o_perm[gw * A + qq[u]] = (uint8_t)pa[u];
+                            for (int u = 0; u < 8; ++u) {
+                                const int q = sub + 4 * u;
+                                if (q < A) S.o_perm[gw * A + q] = (uint8_t)pa[u];
+                            }
 #ifdef CN_STAMPS
                             if (threadIdx.x == 0 && blockIdx.x < 4096) cn_stamp_a[blockIdx.x * CN_NSTAMP + 13] = dbg_it;
 #endif
