@@ -30,12 +30,15 @@ def run(variant, E=4096, N=10, steps=300):
         c.humans.end_goal_changing = False
     if variant == "sf":
         c.humans.policy = "social_force"
-    if variant == "c3":
+    if variant in ("c3", "c3nogoal"):
         N = 25
         c.sim.human_num = N
         c.sim.train_val_sim = ["square_crossing"]
         c.action_space.kinematics = "holonomic"
         c.robot.FOV = c.humans.FOV = 1.0
+        if variant == "c3nogoal":
+            c.humans.random_goal_changing = False
+            c.humans.end_goal_changing = False
     if variant in ("c5a", "c5b", "c5a_nonorm", "c5b_nonorm"):   # the two C5 engines (bench.engines_for)
         c.humans.policy = "orca"
         c.action_space.kinematics = "holonomic"
@@ -95,7 +98,7 @@ def run(variant, E=4096, N=10, steps=300):
         R = R[:live.max() + 1]
         t0r = R[R[:, 0] > 0, 0].min()
         st, en = (R[:, 0] - t0r) * 10, (R[:, 1] - t0r) * 10     # ns
-        kd = variant == "c3"
+        kd = variant in ("c3", "c3nogoal")
         nb = len(R)
         is_step = np.zeros(nb, bool)
         if kd:
@@ -119,16 +122,16 @@ def run(variant, E=4096, N=10, steps=300):
     if (A[:, 14] > A[:, 2]).all():
         sub += [("kd: table", A[:, 15] - A[:, 2]), ("kd: walk", A[:, 14] - A[:, 15]),
                 ("kd: rank+lines", A[:, 7] - A[:, 14])]
-    if variant == "c3":
+    if variant in ("c3", "c3nogoal"):
         it = A[:, 13]
         print("      kd walk iterations (thread 0's human, round 2): median %d max %d mean %.2f" % (np.median(it), it.max(), it.mean()))
         sub = [x for x in sub if not x[0].startswith("p0")]
     for nm, v in sub:
         print("      wave0 %-12s median %8d  max %8d" % (nm, np.median(v), v.max()))
-    if variant not in ("c3",):   # linearProgram3 sub-problems of the workgroup (lp3_tasks): count, cycles B1 -> B2
+    if variant not in ("c3", "c3nogoal"):   # linearProgram3 sub-problems of the workgroup (lp3_tasks): count, cycles B1 -> B2
         cyc = A[:, 23]
         print("      lp3 task rounds (lp3_tasks + replays) cycles: median %d max %d" % (np.median(cyc), cyc.max()))
-    if variant != "c3":   # per-wave ends of phases 0-2 (-DCN_STAMPS lanes 0 / 64 / 128), from the phase start
+    if variant not in ("c3", "c3nogoal"):   # per-wave ends of phases 0-2 (-DCN_STAMPS lanes 0 / 64 / 128), from the phase start
         per = [("p0 wave1 env load+clip+VR", A[:, 16] - A[:, 0]), ("p1 wave0 visibility", A[:, 19] - A[:, 1]),
                ("p1 wave1 reward terms", A[:, 17] - A[:, 1]), ("p1 wave2 robot terms", A[:, 18] - A[:, 1]),
                ("p2 wave1 quads done", A[:, 21] - A[:, 2]), ("p2 wave1 +ladder", A[:, 20] - A[:, 2])]
@@ -158,7 +161,7 @@ def run(variant, E=4096, N=10, steps=300):
                     print("        %d rounds: %4d envs, cycles median %d max %d | walk %d first-tries %d reject-loop %d (mean)" % (
                         r, sel.sum(), np.median(part[sel]), part[sel].max(), goal[sel, k0].mean(), goal[sel, k0 + 1].mean(),
                         goal[sel, k0 + 2].mean()))
-    if variant == "c3":
+    if variant in ("c3", "c3nogoal"):
         L.cn_debug_stamps_c.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         cc = np.zeros(8192 * 4, np.uint64)
         pp = np.zeros(8192 * 2, np.uint64)
