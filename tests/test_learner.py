@@ -404,7 +404,12 @@ def test_c4_shape_update_properties():
         c = cfg()
         torch.manual_seed(11)
         envs = CrowdNavVecEnv(c, E4, c.env.seed, "cuda:0", nenv=E4, phase="train")
-        pol = make_policy(N4, E=E4, T=T4, device="cuda:0")
+        from crowdnav_dsrnn_amd.policy import Policy
+        from tests.helpers import BoxSpace, procedural_state_dict
+
+        pol = Policy({}, BoxSpace((2,)), base="srnn", base_kwargs=c)   # nenv / num_mini_batch rows per minibatch
+        pol.load_state_dict(procedural_state_dict(pol))
+        pol = pol.to("cuda:0")
         agent = PPO(pol, c.ppo.clip_param, c.ppo.epoch, MB, c.ppo.value_loss_coef, c.ppo.entropy_coef,
                     lr=c.training.lr, eps=c.training.eps, max_grad_norm=c.training.max_grad_norm)
         tr = RolloutTrainer(c, envs, pol, agent, deterministic=True, graphs=graphs)
