@@ -98,6 +98,8 @@ def lib():
         L.cn_gru_bias_work_elems.restype = i64
         L.cn_gru_bwd_step_bias.argtypes = [vp, i64, ctypes.c_int] + [vp] * 8
         L.cn_gru_bwd_step_bias.restype = i32
+        L.cn_gru_bwd_step_gates.argtypes = [vp, i64, ctypes.c_int] + [vp] * 7
+        L.cn_gru_bwd_step_gates.restype = i32
         L.cn_gru_bias_reduce.argtypes = [vp, i64, ctypes.c_int] + [vp] * 4
         L.cn_gru_bias_reduce.restype = i32
         L.cn_set_graph_mode.argtypes = [vp, vp, ctypes.c_int]
@@ -133,7 +135,7 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter",
             "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_spatial_attn_fwd",
             "cn_spatial_attn_bwd", "cn_wgrad_work_elems", "cn_wgrad",
-            "cn_gru_bias_blocks", "cn_gru_bwd_step_bias", "cn_gru_bias_work_elems", "cn_gru_bias_reduce",
+            "cn_gru_bias_blocks", "cn_gru_bwd_step_bias", "cn_gru_bwd_step_gates", "cn_gru_bias_work_elems", "cn_gru_bias_reduce",
             "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad",
             "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict",
             "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"]

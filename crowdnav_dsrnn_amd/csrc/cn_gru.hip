@@ -126,6 +126,10 @@ __global__ __launch_bounds__(256) void cn_gru_bwd_kernel(int64_t B, int H, float
 // part [blocks][4H] (row slots summed in order through LDS); cn_gru_bias_reduce adds the partials of all
 // steps in order (deterministic).
 #define CN_GB_RW 16
+// COMB: the gate gradients go once to g = [dn | dr | dz | dhn] per row (4H; dgi's r / z columns equal dgh's,
+// so dgh = g[:, H:4H] and dgi = g[:, 0:3H] with the input weights' rows taken in the order n, r, z) instead of
+// the separate [dr | dz | dn] and [dr | dz | dhn] (6H): 2H fewer floats written per row and step
+template <bool COMB>
 __global__ __launch_bounds__(256) void cn_gru_bwd_bias_kernel(int64_t B, int H, float *__restrict__ acc,
                                                               const float *__restrict__ m_next,
                                                               const float *__restrict__ dout,
@@ -168,12 +172,20 @@ __global__ __launch_bounds__(256) void cn_gru_bwd_bias_kernel(int64_t B, int H, 
         CN_GBWD(x) CN_GBWD(y) CN_GBWD(z) CN_GBWD(w)
 #undef CN_GBWD
         *(float4 *)(acc + b * H + j) = a;
-        *(float4 *)(dgi + b * 3 * H + j) = dr;
-        *(float4 *)(dgi + b * 3 * H + H + j) = dz;
-        *(float4 *)(dgi + b * 3 * H + 2 * H + j) = dn;
-        *(float4 *)(dgh + b * 3 * H + j) = dr;
-        *(float4 *)(dgh + b * 3 * H + H + j) = dz;
-        *(float4 *)(dgh + b * 3 * H + 2 * H + j) = dhn;
+        if (COMB) {
+            float *gr = dgi + b * 4 * H + j;
+            *(float4 *)(gr) = dn;
+            *(float4 *)(gr + H) = dr;
+            *(float4 *)(gr + 2 * H) = dz;
+            *(float4 *)(gr + 3 * H) = dhn;
+        } else {
+            *(float4 *)(dgi + b * 3 * H + j) = dr;
+            *(float4 *)(dgi + b * 3 * H + H + j) = dz;
+            *(float4 *)(dgi + b * 3 * H + 2 * H + j) = dn;
+            *(float4 *)(dgh + b * 3 * H + j) = dr;
+            *(float4 *)(dgh + b * 3 * H + H + j) = dz;
+            *(float4 *)(dgh + b * 3 * H + 2 * H + j) = dhn;
+        }
     }
     red[threadIdx.x][0] = sr; red[threadIdx.x][1] = sz; red[threadIdx.x][2] = sn; red[threadIdx.x][3] = shn;
     __syncthreads();
@@ -471,8 +483,20 @@ int cn_gru_bwd_step_bias(void *stream, int64_t B, int H, float *acc, const float
     if (B <= 0 || !(H == 64 || H == 128 || H == 256)) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step_bias: H in {64, 128, 256}");
     if (!acc || !save || !hm || !dgi || !dgh || !part) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step_bias: null operand");
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
-    hipLaunchKernelGGL(cn_gru_bwd_bias_kernel, dim3((unsigned)cn_gru_bias_blocks(B)), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(cn_gru_bwd_bias_kernel<false>, dim3((unsigned)cn_gru_bias_blocks(B)), dim3(256), 0, (hipStream_t)stream,
                        B, H, acc, m_next, dout, save, hm, dgi, dgh, part);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+int cn_gru_bwd_step_gates(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
+                          const float *save, const float *hm, float *g, float *part)
+{
+    if (B <= 0 || !(H == 64 || H == 128 || H == 256)) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step_gates: H in {64, 128, 256}");
+    if (!acc || !save || !hm || !g || !part) return cn_set_error(CN_EINVAL, "cn_gru_bwd_step_gates: null operand");
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
+    hipLaunchKernelGGL(cn_gru_bwd_bias_kernel<true>, dim3((unsigned)cn_gru_bias_blocks(B)), dim3(256), 0, (hipStream_t)stream,
+                       B, H, acc, m_next, dout, save, hm, g, nullptr, part);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }

@@ -113,7 +113,11 @@ def wgrad(dy, x, chunk=16384):
     if S < 4:
         return dy.t() @ x
     Kc = K // S
-    main = torch.bmm(dy[:S * Kc].view(S, Kc, -1).transpose(1, 2), x[:S * Kc].view(S, Kc, -1)).sum(0)
+
+    def chunks(t):   # (S, Kc, n) view of a row-strided (K, n) matrix (unit column stride)
+        return t.as_strided((S, Kc, t.shape[1]), (Kc * t.stride(0), t.stride(0), t.stride(1)))
+
+    main = torch.bmm(chunks(dy).transpose(1, 2), chunks(x)).sum(0)
     if S * Kc < K:
         main = main + dy[S * Kc:].t() @ x[S * Kc:]
     return main
@@ -223,34 +227,47 @@ class _MaskedGRU(torch.autograd.Function):
         st = _stream(dev)
         acc = dhT.contiguous().clone() if dhT is not None else torch.zeros((B, H), dtype=torch.float32, device=dev)
         dout = dout.contiguous() if dout is not None else None
-        dgi = torch.empty((T, B, 3 * H), dtype=torch.float32, device=dev)
-        dgh = torch.empty((T, B, 3 * H), dtype=torch.float32, device=dev)
-        # bias gradients folded into the step kernel (column sums per 16-row block, reduced once at the end)
+        # bias gradients folded into the step kernel (column sums per 16-row block, reduced once at the end);
+        # the gate gradients stored once per row, g = [dn | dr | dz | dhn] (cn_gru_bwd_step_gates):
+        # dgh = g[:, H:4H], dgi = g[:, 0:3H] in gate order (n, r, z)
         nblk = L.cn_gru_bias_blocks(B) if H in (64, 128, 256) else 0
-        part = torch.empty((T, nblk, 4 * H), dtype=torch.float32, device=dev) if nblk else None
+        if nblk:
+            part = torch.empty((T, nblk, 4 * H), dtype=torch.float32, device=dev)
+            g = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
+        else:
+            dgi = torch.empty((T, B, 3 * H), dtype=torch.float32, device=dev)
+            dgh = torch.empty((T, B, 3 * H), dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
             for t in reversed(range(T)):
                 args = (st, B, H, acc.data_ptr(), None if t + 1 == T else m[t + 1].data_ptr(),
-                        dout[t].data_ptr() if dout is not None else None, save[t].data_ptr(),
-                        hm[t].data_ptr(), dgi[t].data_ptr(), dgh[t].data_ptr())
-                if part is not None:
-                    _lib.check(L.cn_gru_bwd_step_bias(*args, part[t].data_ptr()))
+                        dout[t].data_ptr() if dout is not None else None, save[t].data_ptr(), hm[t].data_ptr())
+                if nblk:
+                    _lib.check(L.cn_gru_bwd_step_gates(*args, g[t].data_ptr(), part[t].data_ptr()))
+                    acc.addmm_(g[t][:, H:], w_hh)
                 else:
-                    _lib.check(L.cn_gru_bwd_step(*args))
-                acc.addmm_(dgh[t], w_hh)
-            if part is not None:
+                    _lib.check(L.cn_gru_bwd_step(*args, dgi[t].data_ptr(), dgh[t].data_ptr()))
+                    acc.addmm_(dgh[t], w_hh)
+            if nblk:
                 db_ih = torch.empty((3 * H,), dtype=torch.float32, device=dev)
                 db_hh = torch.empty((3 * H,), dtype=torch.float32, device=dev)
                 work = torch.empty((L.cn_gru_bias_work_elems(H),), dtype=torch.float32, device=dev)
                 _lib.check(L.cn_gru_bias_reduce(st, T * nblk, H, part.data_ptr(), db_ih.data_ptr(), db_hh.data_ptr(),
                                                 work.data_ptr()))
         dh0 = acc * m[0].unsqueeze(-1)
+        hm2 = hm.reshape(T * B, H)
+        if nblk:
+            g2 = g.view(T * B, 4 * H)
+            dgi_nrz, dgh2 = g2[:, :3 * H], g2[:, H:]
+            w_ih_nrz = torch.cat((w_ih[2 * H:], w_ih[:2 * H]), 0)   # W_ih's rows in gate order n, r, z
+            dx = (dgi_nrz @ w_ih_nrz).reshape(T, B, -1) if ctx.needs_input_grad[0] else None
+            dw = wgrad(dgi_nrz, x2)
+            dw_ih = torch.cat((dw[H:], dw[:H]), 0)                   # back to r, z, n
+            return (dx, dh0, None, dw_ih, wgrad(dgh2, hm2), db_ih, db_hh)
         dgi2 = dgi.reshape(T * B, 3 * H)
         dgh2 = dgh.reshape(T * B, 3 * H)
-        if part is None:
-            db_ih, db_hh = dgi2.sum(0), dgh2.sum(0)
+        db_ih, db_hh = dgi2.sum(0), dgh2.sum(0)
         dx = (dgi2 @ w_ih).reshape(T, B, -1) if ctx.needs_input_grad[0] else None
-        return (dx, dh0, None, wgrad(dgi2, x2), wgrad(dgh2, hm.reshape(T * B, H)), db_ih, db_hh)
+        return (dx, dh0, None, wgrad(dgi2, x2), wgrad(dgh2, hm2), db_ih, db_hh)
 
 
 def masked_gru(x, h0, masks, w_ih, w_hh, b_ih, b_hh):

@@ -264,6 +264,11 @@ int cn_gru_bwd_step(void *stream, int64_t B, int H, float *acc, const float *m_n
 int64_t cn_gru_bias_blocks(int64_t B);
 int cn_gru_bwd_step_bias(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
                          const float *save, const float *hm, float *dgi, float *dgh, float *part);
+/* cn_gru_bwd_step_bias with the gate gradients stored once, g [B][4H] = [dn | dr | dz | dhn] per row:
+ * dgh_t = g[:, H:4H] and dgi_t = g[:, 0:3H] in gate order (n, r, z) (dgi's r / z columns equal dgh's), 2H
+ * fewer floats written per row than the separate dgi / dgh. Same acc and bias partials. */
+int cn_gru_bwd_step_gates(void *stream, int64_t B, int H, float *acc, const float *m_next, const float *dout,
+                          const float *save, const float *hm, float *g, float *part);
 int64_t cn_gru_bias_work_elems(int H);
 int cn_gru_bias_reduce(void *stream, int64_t rows, int H, const float *part, float *db_ih, float *db_hh,
                        float *work);
