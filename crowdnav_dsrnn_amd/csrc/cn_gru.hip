@@ -256,15 +256,19 @@ inline unsigned grid_for(int64_t B, int H) { return (unsigned)((B * (H / 4) + 25
 constexpr int GF_BM = 128, GF_BU = 32, GF_KC = 32, GF_LD = GF_KC + 4;
 typedef float gf_f32x16 __attribute__((ext_vector_type(16)));
 
-__global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(int64_t B, int H, int row_tiles, int unit_tiles,
-                                                              const float *__restrict__ gi,
-                                                              const float *__restrict__ hm,
-                                                              const float *__restrict__ w_hh,
-                                                              const float *__restrict__ b_hh,
-                                                              const float *__restrict__ m_next,
-                                                              float *__restrict__ h_out, float *__restrict__ hm_next,
-                                                              float *__restrict__ save, float *__restrict__ h_out2,
-                                                              int64_t g2, int64_t ld2)
+// One GRU (segment) of a fused-step launch: two independent GRUs with the same H (the DSRNN's spatial and
+// temporal edge RNNs) share one launch, the row tiles of the second following the first's.
+struct GfSeg {
+    int64_t B;
+    const float *gi, *hm, *w_hh, *b_hh, *m_next;
+    float *h_out, *hm_next, *save, *h_out2;
+    int64_t g2, ld2;
+};
+struct GfArgs {
+    GfSeg s0, s1;
+    int rt0, rt_total, unit_tiles, H;
+};
+__global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(const GfArgs P)
 {
     // LDS: one A / B chunk buffer during the K loop, then the three gate accumulators of the tile
     // (sC[g][row][unit], rows padded to LDC = 33) for the epilogue's row-major pass. 50.7 KB in all, so three
@@ -276,9 +280,19 @@ __global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(int64_t B, int H, 
     float *const sA0 = smem, *const sB0 = smem + SA;
     const int bid = blockIdx.x;
     const int xcd = bid & 7, k = bid >> 3;
+    const int unit_tiles = P.unit_tiles, H = P.H;
     const int ut = k % unit_tiles;
-    const int rt = (k / unit_tiles) * 8 + xcd;
-    if (rt >= row_tiles) return;  // grid padding (whole workgroup, before any barrier)
+    int rt = (k / unit_tiles) * 8 + xcd;
+    if (rt >= P.rt_total) return;  // grid padding (whole workgroup, before any barrier)
+    const bool second = rt >= P.rt0;
+    const GfSeg S = second ? P.s1 : P.s0;
+    if (second) rt -= P.rt0;
+    const int64_t B = S.B;
+    const float *__restrict__ gi = S.gi, *__restrict__ hm = S.hm, *__restrict__ w_hh = S.w_hh,
+                                  *__restrict__ b_hh = S.b_hh, *__restrict__ m_next = S.m_next;
+    float *__restrict__ h_out = S.h_out, *__restrict__ hm_next = S.hm_next, *__restrict__ save = S.save,
+                        *__restrict__ h_out2 = S.h_out2;
+    const int64_t g2 = S.g2, ld2 = S.ld2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int64_t row0 = (int64_t)rt * GF_BM;
     const int u0 = ut * GF_BU;
@@ -339,6 +353,14 @@ __global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(int64_t B, int H, 
         for (int e = 0; e < 16; ++e) acc[g][e] = 0.0f;
 
     const int nch = H / GF_KC;
+    float4 eg[4][3], eh[4];
+#define GF_EPI_LOAD()                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                       \
+    {                                                                                    \
+        const float *gib = gi + ar[i] * 3 * H + u0 + lc;                                 \
+        _Pragma("unroll") for (int g = 0; g < 3; ++g) eg[i][g] = *(const float4 *)(gib + g * H); \
+        eh[i] = *(const float4 *)(hm + ar[i] * H + u0 + lc);                             \
+    }
     GF_GLOAD(0)
     GF_LSTORE(0)
     __syncthreads();
@@ -351,14 +373,8 @@ __global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(int64_t B, int H, 
     }
     // last chunk: the epilogue's operands (gi's three gate blocks and hm of this thread's 4 x 4 outputs) are
     // fetched while its MFMAs run
-    float4 eg[4][3], eh[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const float *gib = gi + ar[i] * 3 * H + u0 + lc;
-#pragma unroll
-        for (int g = 0; g < 3; ++g) eg[i][g] = *(const float4 *)(gib + g * H);
-        eh[i] = *(const float4 *)(hm + ar[i] * H + u0 + lc);
-    }
+    GF_EPI_LOAD()
+#undef GF_EPI_LOAD
     GF_MMA(0)
     __syncthreads();  // every wave is done reading the chunk buffers before sC overwrites them
 #undef GF_GLOAD
@@ -386,10 +402,6 @@ __global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(int64_t B, int H, 
         const float4 cz = make_float4(pcz[0], pcz[1], pcz[2], pcz[3]);
         const float *pcn = smem + (2 * GF_BM + row) * LDC + lc;
         const float4 cn = make_float4(pcn[0], pcn[1], pcn[2], pcn[3]);
-#ifdef CN_GF_PROBE_NOEPI  // diagnostic build (tools/gru_fused_probe.hip): the GEMM loop + LDS pass alone
-        *(float4 *)(h_out + b * H + u0 + lc) = make_float4(cr.x + cz.x + cn.x, cr.y, cz.z, cn.w);
-        continue;
-#endif
         const float4 ir = eg[i][0], iz = eg[i][1], in = eg[i][2], hp = eh[i];
         float4 hr, hz, hn, r, z, n, h;
 #define CN_GATE(c)                                 \
@@ -423,6 +435,239 @@ __global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(int64_t B, int H, 
             *(float4 *)(sv + 3 * H) = hn;
         }
     }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused backward step: the recurrent GEMM of step t, acc_t = a_t + g_t[:, H:4H] W_hh (K = 3H; a_t = the
+// direct path dL/dh_t * z_t), on the f32 matrix cores with the gate gradients of step t - 1 in its epilogue:
+//   gacc = acc_t * m_t + dout_{t-1}                       (dL/dh_{t-1})
+//   dn = gacc (1 - z) (1 - n^2), dz = gacc (hm - n) z (1 - z), dr = dn gh_n r (1 - r), dhn = dn r
+//   a_{t-1} = gacc z;  g_{t-1} = [dn | dr | dz | dhn];  column sums of dr | dz | dn | dhn -> part
+// so acc_t never goes to HBM and the backward is one launch per step (cn_gru_bwd_seq). Modes per launch: no
+// GEMM (gk = null: the first step, acc = dL/dh_{T-1} comes in through a) and no gates (g = null: the last
+// step, a <- acc_0 = dL/dhm_0). Same tiling as cn_gru_fused_kernel: 128 rows x 32 hidden units per
+// workgroup, wave w owns rows 32w .. 32w + 31 with one 32x32 accumulator (v_mfma_f32_32x32x2_f32), K in
+// chunks of 32 through double-buffered LDS (46 KB: three workgroups per CU), XCD-aware tile order.
+// The B operand is W_hh^T [H][3H] (row u = unit u's weights over the 3H gate gradients, contiguous in K).
+// ------------------------------------------------------------------------------------------------
+struct GbSeg {
+    int64_t B;
+    const float *gk;      // g_t [B][4H]: the K operand is its columns H .. 4H (dr | dz | dhn); null: no GEMM
+    const float *wt;      // W_hh^T [H][3H]
+    float *a;             // [B][H]: in a_t (or dL/dh_{T-1}), out a_{t-1} (gates) or acc_t (no gates)
+    const float *m_next;  // [B] m_t, or null (= 1)
+    const float *dout;    // [B][H] dL/d out_{t-1}, or null
+    const float *save;    // [B][4H] r | z | n | gh_n of step t - 1
+    const float *hm;      // [B][H] masked state entering step t - 1
+    float *g;             // [B][4H] out g_{t-1}, or null: no gates
+    float *part;          // [row tiles][4H] out: the workgroup's column sums
+};
+struct GbArgs {
+    GbSeg s0, s1;
+    int rt0, rt_total, unit_tiles, H;
+};
+
+__global__ __launch_bounds__(256, 3) void cn_gru_bwd_fused_kernel(const GbArgs P)
+{
+    constexpr int SA = GF_BM * GF_LD, SB = GF_BU * GF_LD, LDC = 33;
+    __shared__ __attribute__((aligned(16))) float smem[2 * (SA + SB)];
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, k = bid >> 3;
+    const int unit_tiles = P.unit_tiles, H = P.H;
+    const int ut = k % unit_tiles;
+    int rt = (k / unit_tiles) * 8 + xcd;
+    if (rt >= P.rt_total) return;  // grid padding (whole workgroup, before any barrier)
+    const bool second = rt >= P.rt0;
+    const GbSeg S = second ? P.s1 : P.s0;
+    if (second) rt -= P.rt0;
+    const int64_t B = S.B;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t row0 = (int64_t)rt * GF_BM;
+    const int u0 = ut * GF_BU;
+    const int lc = (tid & 7) * 4, lr = tid >> 3;
+    const int li = lane & 31, p4 = (lane >> 5) * 4;
+    int64_t ar[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ar[i] = min(row0 + lr + 32 * i, B - 1);
+
+    gf_f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+    // the gate records of the epilogue's 4 x 4 outputs (thread: units u0 + lc .. + 3 of rows lr + 32 i) are
+    // fetched during the last chunk; the other operands (a, dout, hm: one float4 per row each) in the epilogue
+    float4 es[4][4];
+    const bool gates = S.g != nullptr;
+#define GB_EPI_LOAD()                                                                                   \
+    if (gates) {                                                                                        \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
+        {                                                                                               \
+            const float *sv = S.save + ar[i] * 4 * H + u0 + lc;                                         \
+            _Pragma("unroll") for (int q = 0; q < 4; ++q) es[i][q] = *(const float4 *)(sv + q * H);    \
+        }                                                                                               \
+    }
+
+    if (S.gk) {
+        const int K3 = 3 * H, ldg = 4 * H;
+        const float *pa0 = S.gk + ar[0] * ldg + H + lc, *pa1 = S.gk + ar[1] * ldg + H + lc,
+                    *pa2 = S.gk + ar[2] * ldg + H + lc, *pa3 = S.gk + ar[3] * ldg + H + lc;
+        const float *pb = S.wt + (int64_t)(u0 + lr) * K3 + lc;
+        float4 ra0, ra1, ra2, ra3, rb;
+#define GB_GLOAD(kc)                           \
+    ra0 = *(const float4 *)(pa0 + (kc));       \
+    ra1 = *(const float4 *)(pa1 + (kc));       \
+    ra2 = *(const float4 *)(pa2 + (kc));       \
+    ra3 = *(const float4 *)(pa3 + (kc));       \
+    rb = *(const float4 *)(pb + (kc));
+#define GB_LSTORE(buf)                                                                          \
+    {                                                                                           \
+        float *da = smem + (buf) * SA + lr * GF_LD + lc, *db = smem + 2 * SA + (buf) * SB + lr * GF_LD + lc; \
+        *(float4 *)(da) = ra0;                                                                  \
+        *(float4 *)(da + 32 * GF_LD) = ra1;                                                     \
+        *(float4 *)(da + 64 * GF_LD) = ra2;                                                     \
+        *(float4 *)(da + 96 * GF_LD) = ra3;                                                     \
+        *(float4 *)(db) = rb;                                                                   \
+    }
+#define GB_MMA(buf)                                                                             \
+    {                                                                                           \
+        const float *a_base = smem + (buf) * SA + (wave * 32 + li) * GF_LD + p4;                \
+        const float *b_base = smem + 2 * SA + (buf) * SB + li * GF_LD + p4;                     \
+        _Pragma("unroll") for (int c = 0; c < GF_KC / 8; ++c)                                   \
+        {                                                                                       \
+            const float4 av = *(const float4 *)(a_base + 8 * c);                                \
+            const float4 bv = *(const float4 *)(b_base + 8 * c);                                \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.x, bv.x, acc, 0, 0, 0);               \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.y, bv.y, acc, 0, 0, 0);               \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.z, bv.z, acc, 0, 0, 0);               \
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av.w, bv.w, acc, 0, 0, 0);               \
+        }                                                                                       \
+    }
+        const int nch = K3 / GF_KC;
+        GB_GLOAD(0)
+        GB_LSTORE(0)
+        __syncthreads();
+        for (int ch = 0; ch + 1 < nch; ++ch) {
+            GB_GLOAD((ch + 1) * GF_KC)  // in flight during this chunk's MFMAs
+            GB_MMA(ch & 1)
+            GB_LSTORE((ch + 1) & 1)     // the other buffer: its last readers passed the previous barrier
+            __syncthreads();
+        }
+        GB_EPI_LOAD()
+        GB_MMA((nch - 1) & 1)
+        __syncthreads();  // every wave is done reading the chunk buffers before sC overwrites them
+#undef GB_GLOAD
+#undef GB_LSTORE
+#undef GB_MMA
+    } else {
+        GB_EPI_LOAD()
+    }
+#undef GB_EPI_LOAD
+    // accumulator -> LDS (sC [128][LDC]): lane holds unit li of rows (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+    float *const sC = smem;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sC[(wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * LDC + li] = acc[e];
+    __syncthreads();
+
+    float4 sr = make_float4(0.f, 0.f, 0.f, 0.f), sz = sr, sn = sr, shn = sr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = lr + 32 * i;
+        const int64_t b = row0 + row;
+        if (b >= B) continue;
+        const int64_t o = b * H + u0 + lc;
+        const float *pc = sC + row * LDC + lc;
+        const float4 ai = *(const float4 *)(S.a + o);
+        const float4 v = make_float4(pc[0] + ai.x, pc[1] + ai.y, pc[2] + ai.z, pc[3] + ai.w);
+        if (!gates) {
+            *(float4 *)(S.a + o) = v;
+            continue;
+        }
+        const float m = S.m_next ? S.m_next[b] : 1.0f;
+        const float4 d = S.dout ? *(const float4 *)(S.dout + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 hp = *(const float4 *)(S.hm + o);
+        const float4 r = es[i][0], z = es[i][1], n = es[i][2], hn = es[i][3];
+        float4 a, dr, dz, dn, dhn;
+#define CN_GBWD(c)                                                  \
+    {                                                               \
+        const float gc = v.c * m + d.c;                             \
+        const float dnc = gc * (1.0f - z.c) * (1.0f - n.c * n.c);   \
+        const float dzc = gc * (hp.c - n.c) * z.c * (1.0f - z.c);   \
+        const float drc = dnc * hn.c * r.c * (1.0f - r.c);          \
+        a.c = gc * z.c;                                             \
+        dr.c = drc;                                                 \
+        dz.c = dzc;                                                 \
+        dn.c = dnc;                                                 \
+        dhn.c = dnc * r.c;                                          \
+        sr.c += drc; sz.c += dzc; sn.c += dnc; shn.c += dhn.c;      \
+    }
+        CN_GBWD(x) CN_GBWD(y) CN_GBWD(z) CN_GBWD(w)
+#undef CN_GBWD
+        *(float4 *)(S.a + o) = a;
+        float *gr = S.g + b * 4 * H + u0 + lc;
+        *(float4 *)(gr) = dn;
+        *(float4 *)(gr + H) = dr;
+        *(float4 *)(gr + 2 * H) = dz;
+        *(float4 *)(gr + 3 * H) = dhn;
+    }
+    if (!gates) return;
+    // column sums of the tile (32 units x 4 gates) over its 128 rows: thread rows in order through LDS
+    float *const red = smem + GF_BM * LDC;
+    float *rw = red + tid * 16;
+    *(float4 *)(rw) = sr;
+    *(float4 *)(rw + 4) = sz;
+    *(float4 *)(rw + 8) = sn;
+    *(float4 *)(rw + 12) = shn;
+    __syncthreads();
+    if (tid >= 4 * GF_BU) return;
+    const int q = tid / GF_BU, cu = tid - q * GF_BU;
+    const float *src = red + (cu >> 2) * 16 + q * 4 + (cu & 3);
+    float s = 0.0f;
+    for (int r = 0; r < 32; ++r) s += src[r * 8 * 16];
+    S.part[(int64_t)rt * 4 * H + q * H + u0 + cu] = s;
+}
+
+// ------------------------------------------------------------------------------------------------
+// The act() tail of the Box-action policy (distributions.py:74-94 DiagGaussian + FixedNormal, with the
+// reference's operation order and torch's float32 arithmetic): std = exp(0 + logstd) (AddBias on zeros),
+// action = eps * std + mean (sample; eps = torch.randn) or mean (mode), and
+//   log_prob = sum_a [ -((action - mean)^2) / (2 std^2) - log(std) - log(sqrt(2 pi)) ]
+// one thread per env: ~15 tiny torch launches per act() in one (the HIP-graph rollout replays them all).
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cn_gaussian_act_kernel(int64_t E, int A, const float *__restrict__ mean,
+                                                              const float *__restrict__ logstd,
+                                                              const float *__restrict__ eps,
+                                                              float *__restrict__ action, float *__restrict__ logp)
+{
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    const float c = 0.9189385332046727f;   // math.log(math.sqrt(2 * math.pi)) as torch's float32 scalar
+    float lp = 0.0f;
+    for (int a = 0; a < A; ++a) {
+        const float sd = expf(0.0f + logstd[a]);
+        const float mu = mean[e * A + a];
+        const float x = eps ? eps[e * A + a] * sd + mu : mu;
+        action[e * A + a] = x;
+        const float d = x - mu;
+        const float var = sd * sd;
+        const float t = -(d * d) / (2.0f * var) - logf(sd) - c;
+        lp = a ? lp + t : t;
+    }
+    logp[e] = lp;
+}
+
+static int launch_fwd_fused(hipStream_t st, GfArgs &P, int64_t B0, int64_t B1, int H)
+{
+    const int64_t rt0 = (B0 + GF_BM - 1) / GF_BM, rt1 = (B1 + GF_BM - 1) / GF_BM;
+    const int ut = H / GF_BU;
+    const int64_t grid = (rt0 + rt1 + 7) / 8 * 8 * ut;
+    if (grid > 0x7fffffff) return cn_set_error(CN_EINVAL, "fused GRU step: B too large");
+    P.rt0 = (int)rt0;
+    P.rt_total = (int)(rt0 + rt1);
+    P.unit_tiles = ut;
+    P.H = H;
+    (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
+    hipLaunchKernelGGL(cn_gru_fused_kernel, dim3((unsigned)grid), dim3(256), 0, st, P);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }
 
 }  // namespace
@@ -464,15 +709,111 @@ int cn_gru_fwd_fused(void *stream, int64_t B, int H, const float *gi, const floa
         return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: hm, w_hh, gi, b_hh, h_out, hm_next and save must be 16-byte aligned");
     if (h_out2 && (g2 <= 0 || ld2 < g2 * H))
         return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: g2 > 0 and ld2 >= g2 * H required");
-    const int64_t rt = (B + GF_BM - 1) / GF_BM;
-    const int ut = H / GF_BU;
-    const int64_t grid = (rt + 7) / 8 * 8 * ut;
-    if (grid > 0x7fffffff) return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: B too large");
+    GfArgs P{};
+    P.s0 = GfSeg{B, gi, hm, w_hh, b_hh, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2};
+    P.s1 = P.s0;
+    return launch_fwd_fused((hipStream_t)stream, P, B, 0, H);
+}
+
+int cn_gaussian_act(void *stream, int64_t E, int A, const float *mean, const float *logstd, const float *eps,
+                    float *action, float *logp)
+{
+    if (E <= 0 || A <= 0 || A > 64) return cn_set_error(CN_EINVAL, "cn_gaussian_act: E > 0 and 0 < A <= 64 required");
+    if (!mean || !logstd || !action || !logp) return cn_set_error(CN_EINVAL, "cn_gaussian_act: null operand");
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
-    hipLaunchKernelGGL(cn_gru_fused_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, B, H, (int)rt, ut,
-                       gi, hm, w_hh, b_hh, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2);
+    hipLaunchKernelGGL(cn_gaussian_act_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       E, A, mean, logstd, eps, action, logp);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
+}
+
+int64_t cn_gru_seq_tiles(int64_t B) { return (B + GF_BM - 1) / GF_BM; }
+
+static bool aligned16(std::initializer_list<const void *> ps)
+{
+    for (const void *p : ps)
+        if ((uintptr_t)p & 15) return false;
+    return true;
+}
+
+int cn_gru_fwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_fwd *segs)
+{
+    if (T <= 0 || H <= 0 || H % GF_BU || nseg < 1 || nseg > 2 || !segs)
+        return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: T > 0, H % 32 == 0 and 1 <= nseg <= 2 required");
+    for (int s = 0; s < nseg; ++s) {
+        const cn_gru_seq_fwd &q = segs[s];
+        if (q.B <= 0 || q.nh < 1 || q.nh > T) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: B > 0 and 1 <= nh <= T required");
+        if (!q.gi || !q.w_hh || !q.b_hh || !q.m || !q.out || !q.hm) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: null operand");
+        if (!aligned16({q.gi, q.w_hh, q.b_hh, q.out, q.hm, q.save}))
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: gi, w_hh, b_hh, out, hm and save must be 16-byte aligned");
+    }
+    const int64_t B1 = nseg > 1 ? segs[1].B : 0;
+    for (int t = 0; t < T; ++t) {
+        GfArgs P{};
+        for (int s = 0; s < nseg; ++s) {
+            const cn_gru_seq_fwd &q = segs[s];
+            const bool last = t + 1 == T;
+            const int64_t BH = q.B * H;
+            GfSeg g{q.B, q.gi + t * 3 * BH, q.hm + (t % q.nh) * BH, q.w_hh, q.b_hh,
+                    last ? nullptr : q.m + (t + 1) * q.B, q.out + t * BH,
+                    last ? nullptr : q.hm + ((t + 1) % q.nh) * BH, q.save ? q.save + t * 4 * BH : nullptr, nullptr,
+                    1, 0};
+            (s ? P.s1 : P.s0) = g;
+        }
+        if (nseg == 1) P.s1 = P.s0;
+        const int rc = launch_fwd_fused((hipStream_t)stream, P, segs[0].B, B1, H);
+        if (rc) return rc;
+    }
+    return CN_OK;
+}
+
+int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs)
+{
+    if (T <= 0 || H <= 0 || H % GF_BU || nseg < 1 || nseg > 2 || !segs)
+        return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: T > 0, H % 32 == 0 and 1 <= nseg <= 2 required");
+    for (int s = 0; s < nseg; ++s) {
+        const cn_gru_seq_bwd &q = segs[s];
+        if (q.B <= 0) return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: B > 0 required");
+        if (!q.w_hh_t || !q.m || !q.save || !q.hm || !q.acc || !q.g || !q.part)
+            return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: null operand");
+        if (!aligned16({q.w_hh_t, q.dout, q.save, q.hm, q.acc, q.g}))
+            return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: w_hh_t, dout, save, hm, acc and g must be 16-byte aligned");
+    }
+    const int ut = H / GF_BU;
+    const int64_t rt0 = cn_gru_seq_tiles(segs[0].B), rt1 = nseg > 1 ? cn_gru_seq_tiles(segs[1].B) : 0;
+    const int64_t grid = (rt0 + rt1 + 7) / 8 * 8 * ut;
+    if (grid > 0x7fffffff) return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: B too large");
+    // launch j = 0 .. T: the GEMM of step T - j (none at j = 0) and the gates of step T - 1 - j (none at j = T)
+    for (int j = 0; j <= T; ++j) {
+        GbArgs P{};
+        P.rt0 = (int)rt0;
+        P.rt_total = (int)(rt0 + rt1);
+        P.unit_tiles = ut;
+        P.H = H;
+        for (int s = 0; s < nseg; ++s) {
+            const cn_gru_seq_bwd &q = segs[s];
+            const int64_t BH = q.B * H, rt = s ? rt1 : rt0;
+            const int tk = T - j, tg = T - 1 - j;
+            const bool gates = tg >= 0;
+            GbSeg g{q.B,
+                    j ? q.g + tk * 4 * BH : nullptr,
+                    q.w_hh_t,
+                    q.acc,
+                    (gates && tg + 1 < T) ? q.m + (tg + 1) * q.B : nullptr,
+                    (gates && q.dout) ? q.dout + tg * BH : nullptr,
+                    gates ? q.save + tg * 4 * BH : nullptr,
+                    gates ? q.hm + tg * BH : nullptr,
+                    gates ? q.g + tg * 4 * BH : nullptr,
+                    gates ? q.part + tg * rt * 4 * H : nullptr};
+            (s ? P.s1 : P.s0) = g;
+        }
+        if (nseg == 1) P.s1 = P.s0;
+        (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
+        hipLaunchKernelGGL(cn_gru_bwd_fused_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, P);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return cn_set_error(CN_EHIP, hipGetErrorString(e));
+    }
+    return CN_OK;
 }
 
 int64_t cn_gru_bias_blocks(int64_t B) { return (B + CN_GB_RW - 1) / CN_GB_RW; }

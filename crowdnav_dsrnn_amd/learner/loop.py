@@ -26,6 +26,7 @@ class RolloutTrainer:
             graphs = envs.engine.device.type == "cuda" and os.environ.get("CN_NO_GRAPHS", "") in ("", "0")
         self.graphs = bool(graphs)
         self._graph, self._warm, self._ep = None, False, None
+        self._ones = self._ep_ret = None
         self.envs = envs
         self.ac = actor_critic
         self.agent = agent
@@ -56,19 +57,26 @@ class RolloutTrainer:
         self.update_index = 0
 
     def _rollout(self, ep_sum, ep_cnt):
+        """num_steps env steps. Per step: act, cn_step, the storage writes (one multi-tensor copy) and one
+        kernel of episode bookkeeping (the returns of the episodes that ended); the episode count and sum
+        are reduced once after the loop (from the stored masks: mask 0 <=> done)."""
         r = self.rollouts
-        for step in range(r.num_steps):
+        T = r.num_steps
+        if self._ones is None or self._ones.shape[0] != self.envs.num_envs:
+            self._ones = torch.ones((self.envs.num_envs, 1), device=self.device)
+            self._ep_ret = torch.zeros((T, self.envs.num_envs), dtype=torch.float64, device=self.device)
+        for step in range(T):
             obs_s = {k: v[step] for k, v in r.obs.items()} if isinstance(r.obs, dict) else r.obs[step]
             hxs_s = r.hidden(step)
             # the new recurrent state goes straight into the storage slot insert() would copy it to
             value, action, logp, hxs = self.ac.act(obs_s, hxs_s, r.masks[step], deterministic=self.deterministic,
                                                    **({"out_hxs": r.hidden_slot()} if self.srnn else {}))
             obs, reward, done, _, _, ep_ret, _ = self.envs.step_device(action)
-            masks = (1.0 - done.float()).unsqueeze(1)
-            r.insert(obs, hxs, action, logp, value, reward.unsqueeze(1), masks, torch.ones_like(masks))
-            d = done.bool()
-            ep_sum += torch.where(d, ep_ret, torch.zeros_like(ep_ret)).sum()
-            ep_cnt += d.sum()
+            masks = torch.rsub(done.unsqueeze(1), 1.0)   # 1 - done as float32 (one kernel)
+            r.insert(obs, hxs, action, logp, value, reward.unsqueeze(1), masks, self._ones)
+            torch.mul(ep_ret, done, out=self._ep_ret[step])   # Monitor return of the episodes that ended
+        ep_sum += self._ep_ret.sum()
+        ep_cnt += (r.masks[1:] == 0).sum()   # (insert() filled slots 1 .. T of this rollout)
 
     @torch.no_grad()
     def collect(self):
@@ -110,8 +118,8 @@ class RolloutTrainer:
 
     def update(self):
         """One rollout + PPO update. rollout_s / update_s are GPU time between HIP events recorded on the
-        current stream (the side streams of the temporal GRU and the mixed engine fork from and join back to
-        it, so their work lies between the events); the update's one host sync (the losses) makes them
+        current stream (the mixed engine's side streams fork from and join back to it, so their work lies
+        between the events); the update's one host sync (the losses) makes them
         readable at the end."""
         c = self.config
         if c.training.use_linear_lr_decay:   # train.py:216-222, before the rollout of update j

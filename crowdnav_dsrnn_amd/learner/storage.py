@@ -61,6 +61,17 @@ def _raw(v):
     return v.t if isinstance(v, CompactSteps) else v
 
 
+def _copy_all(dst, src):
+    """dst[i].copy_(src[i]) for all i: one multi-tensor kernel when every pair has the same shape and
+    dtype (the rollout's storage writes: one launch per step instead of ~10), else one copy each."""
+    same = all(d.shape == x.shape and d.dtype == x.dtype and d.device == x.device for d, x in zip(dst, src))
+    if same and dst and dst[0].is_cuda:
+        torch._foreach_copy_(dst, src)
+    else:
+        for d, x in zip(dst, src):
+            d.copy_(x)
+
+
 def _flatten_helper(T, N, x):
     if isinstance(x, dict):
         return {k: v.reshape(T * N, *v.shape[2:]) for k, v in x.items()}
@@ -107,18 +118,17 @@ class SRNNRolloutStorage:
     def insert(self, obs, recurrent_hidden_states, actions, action_log_probs, value_preds, rewards, masks,
                bad_masks):
         s = self.step
-        for k in self.obs:
-            self.obs[k][s + 1].copy_(obs[k])
+        dst = [self.obs[k][s + 1] for k in self.obs]
+        src = [obs[k] for k in self.obs]
         for k in recurrent_hidden_states:
-            dst = self.recurrent_hidden_states[k][s + 1]
-            if recurrent_hidden_states[k].data_ptr() != dst.data_ptr():   # act(out_hxs=hidden_slot()) wrote it
-                dst.copy_(recurrent_hidden_states[k])
-        self.actions[s].copy_(actions)
-        self.action_log_probs[s].copy_(action_log_probs)
-        self.value_preds[s].copy_(value_preds)
-        self.rewards[s].copy_(rewards)
-        self.masks[s + 1].copy_(masks)
-        self.bad_masks[s + 1].copy_(bad_masks)
+            d = self.recurrent_hidden_states[k][s + 1]
+            if recurrent_hidden_states[k].data_ptr() != d.data_ptr():   # act(out_hxs=hidden_slot()) wrote it
+                dst.append(d)
+                src.append(recurrent_hidden_states[k])
+        dst += [self.actions[s], self.action_log_probs[s], self.value_preds[s], self.rewards[s], self.masks[s + 1],
+                self.bad_masks[s + 1]]
+        src += [actions, action_log_probs, value_preds, rewards, masks, bad_masks]
+        _copy_all(dst, src)
         self.step = (s + 1) % self.num_steps
 
     def hidden(self, step):

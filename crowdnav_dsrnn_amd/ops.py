@@ -270,14 +270,144 @@ class _MaskedGRU(torch.autograd.Function):
         return (dx, dh0, None, wgrad(dgi2, x2), wgrad(dgh2, hm2), db_ih, db_hh)
 
 
+def _a16(t):
+    """t contiguous fp32 with a 16-byte aligned base (the sequence kernels' float4 accesses)."""
+    t = _c(t)
+    return t if t.data_ptr() % 16 == 0 else t.clone()
+
+
+class _MaskedGRUSeq(torch.autograd.Function):
+    """srnn_model.py:52-104 for one or two GRUs of the same T and H (H % 32 == 0) at once: the T-step loops
+    run in native code (cn_gru_fwd_seq / cn_gru_bwd_seq, one launch per step for both GRUs: the DSRNN's
+    spatial and temporal edge RNNs share every launch instead of running on two streams). Forward per GRU:
+    gi = x W_ih^T + b_ih as one GEMM over all T*B rows, then the fused recurrent steps (cn_gru_fwd_fused's
+    kernel). Backward: T + 1 launches of the fused recurrent-GEMM + gate-gradient kernel, then the weight /
+    input gradients as single GEMMs over all T*B rows and the bias partials reduced in a fixed order.
+    Inputs: nseg, then per GRU (x, h0, masks, w_ih, w_hh, b_ih, b_hh); outputs per GRU (out, h_T)."""
+
+    @staticmethod
+    def forward(ctx, nseg, *args):
+        segs = [args[7 * i:7 * i + 7] for i in range(nseg)]
+        need = any(ctx.needs_input_grad)
+        L = _lib.lib()
+        T, H = segs[0][0].shape[0], segs[0][4].shape[1]
+        dev = segs[0][0].device
+        fs = (_lib.GruSeqFwd * nseg)()
+        outs, saved, rows = [], [], 0
+        for i, (x, h0, masks, w_ih, w_hh, b_ih, b_hh) in enumerate(segs):
+            if x.shape[0] != T or w_hh.shape[1] != H:
+                raise ValueError("masked_gru_group: every GRU needs the same T and H")
+            B, F = x.shape[1], x.shape[2]
+            x2 = _c(x).reshape(T * B, F)
+            m = _c(masks).reshape(T, B)
+            gi = torch.addmm(b_ih, x2, w_ih.t())
+            out = torch.empty((T, B, H), dtype=torch.float32, device=dev)
+            nh = T if need else min(T, 2)
+            hm = torch.empty((nh, B, H), dtype=torch.float32, device=dev)
+            torch.mul(h0, m[0].unsqueeze(-1), out=hm[0])
+            save = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev) if need else None
+            whh, bhh = _a16(w_hh), _a16(b_hh)
+            fs[i] = _lib.GruSeqFwd(B, gi.data_ptr(), whh.data_ptr(), bhh.data_ptr(), m.data_ptr(), out.data_ptr(),
+                                   hm.data_ptr(), save.data_ptr() if save is not None else None, nh)
+            outs += [out, gi, whh, bhh]
+            saved += [x2, m, w_ih, w_hh, hm, save]
+            rows += B
+        timing = FUSED_TIMING if (FUSED_TIMING is not None and rows >= FUSED_TIMING_MIN_ROWS) else None
+        if timing is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        with torch.cuda.device(dev):
+            _lib.check(L.cn_gru_fwd_seq(_stream(dev), T, H, nseg, fs))
+        if timing is not None:
+            ev1.record()
+            timing.append((rows, H, T, ev0, ev1))
+        ctx.nseg = nseg
+        if need:
+            ctx.save_for_backward(*saved)
+        res = []
+        for i in range(nseg):
+            out = outs[4 * i]
+            res += [out, out[-1].clone()]
+        return tuple(res)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        nseg = ctx.nseg
+        sv = ctx.saved_tensors
+        L = _lib.lib()
+        dev = sv[0].device
+        st = _stream(dev)
+        bs = (_lib.GruSeqBwd * nseg)()
+        keep = []
+        T, H = sv[4].shape[0], sv[4].shape[2]
+        for i in range(nseg):
+            x2, m, w_ih, w_hh, hm, save = sv[6 * i:6 * i + 6]
+            dout, dhT = grads[2 * i], grads[2 * i + 1]
+            B = hm.shape[1]
+            acc = dhT.float().clone(memory_format=torch.contiguous_format) if dhT is not None else \
+                torch.zeros((B, H), dtype=torch.float32, device=dev)
+            acc = _a16(acc)
+            dout = _a16(dout) if dout is not None else None
+            rt = L.cn_gru_seq_tiles(B)
+            g = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
+            part = torch.empty((T, rt, 4 * H), dtype=torch.float32, device=dev)
+            wt = w_hh.t().contiguous()
+            bs[i] = _lib.GruSeqBwd(B, wt.data_ptr(), m.data_ptr(), dout.data_ptr() if dout is not None else None,
+                                   save.data_ptr(), hm.data_ptr(), acc.data_ptr(), g.data_ptr(), part.data_ptr())
+            keep.append((acc, dout, g, part, wt, rt))
+        with torch.cuda.device(dev):
+            _lib.check(L.cn_gru_bwd_seq(st, T, H, nseg, bs))
+            res = [None]
+            for i in range(nseg):
+                x2, m, w_ih, w_hh, hm, save = sv[6 * i:6 * i + 6]
+                acc, _, g, part, _, rt = keep[i]
+                B = hm.shape[1]
+                db_ih = torch.empty((3 * H,), dtype=torch.float32, device=dev)
+                db_hh = torch.empty((3 * H,), dtype=torch.float32, device=dev)
+                work = torch.empty((L.cn_gru_bias_work_elems(H),), dtype=torch.float32, device=dev)
+                _lib.check(L.cn_gru_bias_reduce(st, T * rt, H, part.data_ptr(), db_ih.data_ptr(), db_hh.data_ptr(),
+                                                work.data_ptr()))
+                dh0 = acc * m[0].unsqueeze(-1)
+                g2 = g.view(T * B, 4 * H)
+                dgi_nrz, dgh2 = g2[:, :3 * H], g2[:, H:]
+                idx = 7 * i + 1   # needs_input_grad index of this GRU's x (after nseg)
+                dx = None
+                if ctx.needs_input_grad[idx]:
+                    w_ih_nrz = torch.cat((w_ih[2 * H:], w_ih[:2 * H]), 0)   # W_ih's rows in gate order n, r, z
+                    dx = (dgi_nrz @ w_ih_nrz).reshape(T, B, -1)
+                dw = wgrad(dgi_nrz, x2)
+                dw_ih = torch.cat((dw[H:], dw[:H]), 0)                       # back to r, z, n
+                res += [dx, dh0, None, dw_ih, wgrad(dgh2, hm.reshape(T * B, H)), db_ih, db_hh]
+        return tuple(res)
+
+
 def masked_gru(x, h0, masks, w_ih, w_hh, b_ih, b_hh):
-    """x (T,B,F), h0 (B,H), masks (T,B) -> out (T,B,H), h_T (B,H); the weights of a 1-layer nn.GRU."""
+    """x (T,B,F), h0 (B,H), masks (T,B) -> out (T,B,H), h_T (B,H); the weights of a 1-layer nn.GRU.
+    H % 32 == 0: the native sequence kernels (_MaskedGRUSeq); otherwise per-step launches (_MaskedGRU)."""
     if not x.is_cuda:
         raise EdgeFeaturesUnavailable("the DSRNN GRUs run only through the HIP step kernels (cn_gru_*); "
                                       "tensors are on %s" % x.device)
     if x.dtype != torch.float32 or w_hh.shape[1] % 4:
         raise ValueError("masked_gru: fp32 operands and a hidden size divisible by 4 required")
+    if w_hh.shape[1] % 32 == 0:
+        return _MaskedGRUSeq.apply(1, x, h0, masks, w_ih, w_hh, b_ih, b_hh)
     return _MaskedGRU.apply(x, h0, masks, w_ih, w_hh, b_ih, b_hh)
+
+
+def masked_gru_group(*grus):
+    """Two (or one) independent masked GRUs of the same T and H (H % 32 == 0) in shared launches: each
+    argument is (x, h0, masks, w_ih, w_hh, b_ih, b_hh) as for masked_gru; returns ((out, h_T), ...)."""
+    if not 1 <= len(grus) <= 2:
+        raise ValueError("masked_gru_group: one or two GRUs")
+    for gr in grus:
+        if not gr[0].is_cuda:
+            raise EdgeFeaturesUnavailable("the DSRNN GRUs run only through the HIP step kernels (cn_gru_*); "
+                                          "tensors are on %s" % gr[0].device)
+        if gr[0].dtype != torch.float32 or gr[4].shape[1] % 32:
+            raise ValueError("masked_gru_group: fp32 operands and a hidden size divisible by 32 required")
+    flat = [t for gr in grus for t in gr]
+    r = _MaskedGRUSeq.apply(len(grus), *flat)
+    return tuple((r[2 * i], r[2 * i + 1]) for i in range(len(grus)))
 
 
 def gru_infer_step(x, h0, m, w_ih, w_hh, b_ih, b_hh, dest):
@@ -317,6 +447,24 @@ def gru_infer_step(x, h0, m, w_ih, w_hh, b_ih, b_hh, dest):
                                                           hm.data_ptr(), None, out.data_ptr(), None, None, d_ptr, G,
                                                           ld))
     return out
+
+
+def gaussian_act(mean, logstd, deterministic=False):
+    """The no-grad act() tail of DiagGaussian (distributions.py:74-94) in one launch: returns
+    (action, log_prob) with action = mean (deterministic) or eps * exp(logstd) + mean, eps = torch.randn
+    (the same draw FixedNormal.sample makes), log_prob summed over the action dims (cn_gaussian_act)."""
+    if not mean.is_cuda:
+        raise EdgeFeaturesUnavailable("gaussian_act runs only as the HIP kernel (tensors are on %s)" % mean.device)
+    mean = _c(mean)
+    E, A = mean.shape
+    eps = None if deterministic else torch.randn((E, A), dtype=mean.dtype, device=mean.device)
+    action = torch.empty_like(mean)
+    logp = torch.empty((E, 1), dtype=torch.float32, device=mean.device)
+    with torch.cuda.device(mean.device):
+        _lib.check(_lib.lib().cn_gaussian_act(_stream(mean.device), E, A, mean.data_ptr(), _c(logstd).data_ptr(),
+                                              eps.data_ptr() if eps is not None else None, action.data_ptr(),
+                                              logp.data_ptr()))
+    return action, logp
 
 
 class _AttnPool(torch.autograd.Function):

@@ -6,8 +6,10 @@ API and return values as in the reference:
   evaluate_actions(inputs, rnn_hxs, masks, action) -> value, log_prob, entropy, rnn_hxs
 `base.nenv` is writable (test.py:199) and `base.human_num` readable (evaluation.py:34).
 """
+import torch
 import torch.nn as nn
 
+from .. import ops
 from .convgru_model import ConvGRU
 from .distributions import DiagGaussian
 from .srnn_model import SRNN
@@ -45,6 +47,12 @@ class Policy(nn.Module):
     def act(self, inputs, rnn_hxs, masks, deterministic=False, out_hxs=None):
         """out_hxs (optional, srnn, no-grad): tensors that receive the new recurrent state (SRNN.forward)."""
         value, actor_features, rnn_hxs = self._infer(inputs, rnn_hxs, masks, out_hxs)
+        if actor_features.is_cuda and not torch.is_grad_enabled() and isinstance(self.dist, DiagGaussian):
+            # sample / mode and log_probs of the same distribution in one launch (ops.gaussian_act)
+            d = self.dist
+            action, action_log_probs = ops.gaussian_act(d.fc_mean(actor_features), d.logstd._bias.view(-1),
+                                                        deterministic)
+            return value, action, action_log_probs, rnn_hxs
         dist = self.dist(actor_features)
         action = dist.mode() if deterministic else dist.sample()
         action_log_probs = dist.log_probs(action)

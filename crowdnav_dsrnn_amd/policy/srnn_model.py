@@ -8,9 +8,10 @@ checkpoints (data/example_model*/checkpoints/*.pt) one to one. The compute is or
     edges (srnn_model.py:210-211), SRNN.robot_linear (:466) and HumanNodeRNN.encoder_linear + ReLU
     (:160-161) — run as ONE fused HIP kernel (`crowdnav_dsrnn_amd.ops.edge_features`) over every env
     (and time step) instead of four small GEMM launches;
-  * the GRUs are torch.nn.GRU on ROCm (MIOpen); the recurrent masks are applied per step on the device
-    (no host synchronisation), which equals the reference's any-zero segmentation
-    (srnn_model.py:52-104): inside a segment every mask is 1;
+  * the GRUs keep torch.nn.GRU's parameters but run as the native mask-segmented sequence kernels
+    (`ops.masked_gru` / `ops.masked_gru_group`; the spatial and temporal edge RNNs share launches): the
+    recurrent masks are applied per step on the device (no host synchronisation), which equals the
+    reference's any-zero segmentation (srnn_model.py:52-104): inside a segment every mask is 1;
   * the spatial-edge attention is batched over envs, humans and time steps.
 """
 import numpy as np
@@ -185,24 +186,20 @@ class SRNN(nn.Module):
         h_node = rnn_hxs["human_node_rnn"].reshape(B, -1)
         H = h_edge.shape[-1]
 
-        # the temporal and spatial edge RNNs are independent: the temporal one (B rows per step, too few to
-        # fill the GPU) runs on a side stream beside the spatial one (B*N rows); autograd runs each backward
-        # on its forward's stream, so the two overlap there as well
-        side = self._side_stream(te) if T > 1 else None
-        if side is not None:
-            main = torch.cuda.current_stream(te.device)
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                out_t, h_t = self.humanhumanEdgeRNN_temporal(te.reshape(T, B, 64), h_edge[:, 0, :], m)
-        else:
-            out_t, h_t = self.humanhumanEdgeRNN_temporal(te.reshape(T, B, 64), h_edge[:, 0, :], m)
+        # the temporal and spatial edge RNNs are independent and have the same sizes: their rows (B and B*N per
+        # step) share every step's launch (ops.masked_gru_group; the temporal RNN alone cannot fill the GPU)
         m_s = m.unsqueeze(-1).expand(T, B, N).reshape(T, B * N)
-        out_s, h_s = self.humanhumanEdgeRNN_spatial(se.reshape(T, B * N, 64), h_edge[:, 1:, :].reshape(B * N, H), m_s)
+        x_s, h0_s = se.reshape(T, B * N, 64), h_edge[:, 1:, :].reshape(B * N, H)
+        x_t, h0_t = te.reshape(T, B, 64), h_edge[:, 0, :]
+        if te.is_cuda and H % 32 == 0:
+            gs, gt = self.humanhumanEdgeRNN_spatial.gru, self.humanhumanEdgeRNN_temporal.gru
+            (out_s, h_s), (out_t, h_t) = ops.masked_gru_group(
+                (x_s, h0_s, m_s, gs.weight_ih_l0, gs.weight_hh_l0, gs.bias_ih_l0, gs.bias_hh_l0),
+                (x_t, h0_t, m, gt.weight_ih_l0, gt.weight_hh_l0, gt.bias_ih_l0, gt.bias_hh_l0))
+        else:
+            out_t, h_t = self.humanhumanEdgeRNN_temporal(x_t, h0_t, m)
+            out_s, h_s = self.humanhumanEdgeRNN_spatial(x_s, h0_s, m_s)
         out_s = out_s.reshape(T, B, N, H)
-        if side is not None:
-            main.wait_stream(side)
-            out_t.record_stream(main)   # allocated on the side stream, consumed here
-            h_t.record_stream(main)
         weighted, _ = self.attn(out_t, out_s)
         outputs, h_n = self.humanNodeRNN(ne.reshape(T, B, 64), out_t, weighted, h_node, m)
 
@@ -213,15 +210,6 @@ class SRNN(nn.Module):
         if infer:
             return self.critic_linear(hidden_critic).squeeze(0), hidden_actor.squeeze(0), rnn_hxs
         return self.critic_linear(hidden_critic).view(-1, 1), hidden_actor.view(-1, self.output_size), rnn_hxs
-
-    def _side_stream(self, t):
-        if not t.is_cuda:
-            return None
-        st = getattr(self, "_side", None)
-        if st is None or st.device != t.device:
-            st = torch.cuda.Stream(device=t.device)
-            self._side = st
-        return st
 
     def _infer_step(self, inputs, rnn_hxs, masks, out_hxs):
         """The act() step without autograd: same arithmetic as the T = 1 path of forward(), but the GRUs

@@ -22,8 +22,12 @@
  *   cn_gru_fwd_step / cn_gru_bwd_step ⟵ one time step of the mask-segmented GRU
  *                   (srnn_model.py:52-104 RNNBase._forward_gru, torch nn.GRU cell math) and its gradient;
  *                   cn_gru_fwd_fused runs the recurrent GEMM hm W_hh^T on the f32 MFMA with the gates in its
- *                   epilogue (the forward's per-step kernel); x W_ih^T over all steps and the backward's
- *                   dgh W_hh remain library GEMMs
+ *                   epilogue (the forward's per-step kernel); cn_gru_fwd_seq / cn_gru_bwd_seq run whole
+ *                   sequences (up to two GRUs per launch; the backward's dgh W_hh on the MFMA with the gate
+ *                   gradients in its epilogue); x W_ih^T and the weight gradients over all steps remain
+ *                   library GEMMs
+ *   cn_gaussian_act ⟵ the act() tail of DiagGaussian / FixedNormal (distributions.py:36-94): sample or
+ *                   mode and the summed log-probability
  *   cn_orca_predict / cn_orca_predict_kd / cn_social_force_predict ⟵ the agent policy plugin
  *                   policy_factory[name](config).predict(JointState) (crowd_nav/policy/policy_factory.py:1-17)
  *   cn_lidar_obs     ⟵ CrowdSimDict.generate_ob's 'convgru' observation (crowd_sim_dict.py:96-101) with
@@ -272,6 +276,53 @@ int cn_gru_bwd_step_gates(void *stream, int64_t B, int H, float *acc, const floa
 int64_t cn_gru_bias_work_elems(int H);
 int cn_gru_bias_reduce(void *stream, int64_t rows, int H, const float *part, float *db_ih, float *db_hh,
                        float *work);
+
+/* The act() tail of the Box-action policy (distributions.py:74-94: DiagGaussian with AddBias(zeros) log-std,
+ * FixedNormal.sample / .mode and .log_probs) for E envs in one launch: std = exp(logstd) [A],
+ * action = eps * std + mean (eps [E][A] from the caller's N(0, 1) draw) or mean when eps = NULL,
+ * logp [E] = sum over the A dims of the Normal log-density of action, in torch's float32 operation order.
+ * mean, eps, action: [E][A]; A <= 64. */
+int cn_gaussian_act(void *stream, int64_t E, int A, const float *mean, const float *logstd, const float *eps,
+                    float *action, float *logp);
+
+/* Whole sequences: the T-step loops of srnn_model.py:52-104's nn.GRU (forward) and of its autograd backward
+ * issued from native code, one launch per step for up to two independent GRUs of the same H at once (the
+ * DSRNN's spatial and temporal edge RNNs, srnn_model.py:455-460; their rows share each launch). H % 32 == 0;
+ * every array 16-byte aligned with rows contiguous; 1 <= nseg <= 2. */
+typedef struct cn_gru_seq_fwd {
+    int64_t B;           /* rows */
+    const float *gi;     /* [T][B][3H] = x W_ih^T + b_ih */
+    const float *w_hh;   /* [3H][H] (weight_hh_l0) */
+    const float *b_hh;   /* [3H] */
+    const float *m;      /* [T][B] masks */
+    float *out;          /* [T][B][H] outputs */
+    float *hm;           /* [nh][B][H] masked states: hm[0] = h0 * m[0] (caller); step t reads hm[t % nh] and
+                            writes hm[(t + 1) % nh] = h_t * m[t + 1] (nh = T keeps all of them for the backward) */
+    float *save;         /* [T][B][4H] r | z | n | gh_n per step for the backward, or NULL */
+    int64_t nh;          /* 1 <= nh <= T */
+} cn_gru_seq_fwd;
+/* cn_gru_fwd_fused for t = 0 .. T - 1 (same arithmetic per row and step). */
+int cn_gru_fwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_fwd *segs);
+
+typedef struct cn_gru_seq_bwd {
+    int64_t B;
+    const float *w_hh_t; /* [H][3H] = weight_hh_l0 transposed */
+    const float *m;      /* [T][B] masks */
+    const float *dout;   /* [T][B][H] dL/d out, or NULL */
+    const float *save;   /* [T][B][4H] and */
+    const float *hm;     /* [T][B][H] as written by cn_gru_fwd_seq (nh = T) */
+    float *acc;          /* [B][H] in: dL/dh_{T-1} through the final state (zeros if unused);
+                            out: dL/d hm_0 (the caller multiplies by m[0] for dL/dh0) */
+    float *g;            /* [T][B][4H] out: dn | dr | dz | dhn per step (dgh_t = g[t][:, H:4H], dgi_t = g[t][:, 0:3H]
+                            in gate order n, r, z) */
+    float *part;         /* [T][cn_gru_seq_tiles(B)][4H] out: bias partials for cn_gru_bias_reduce
+                            (rows = T * cn_gru_seq_tiles(B)) */
+} cn_gru_seq_bwd;
+int64_t cn_gru_seq_tiles(int64_t B);
+/* The backward of cn_gru_fwd_seq: T + 1 launches of one fused kernel, each the recurrent GEMM
+ * acc_t = a_t + dgh_t W_hh of one step on the f32 matrix cores with the gate gradients of the step before in
+ * its epilogue (cn_gru_bwd_step_gates' arithmetic); replaces the per-step cn_gru_bwd_step_gates + GEMM pair. */
+int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs);
 
 /* The ConvGRU observation row of every env, obs [E][7 + beams] float32:
  *   [clip(robot (px, py, radius, gx, gy, v_pref, theta) / max_range, 0, 1), scan].

@@ -34,6 +34,30 @@ def test_library_exports_every_declared_symbol(L):
         assert hasattr(L, sym), sym
 
 
+@pytest.mark.parametrize("cname,py", [("cn_gru_seq_fwd", _lib.GruSeqFwd), ("cn_gru_seq_bwd", _lib.GruSeqBwd)])
+def test_gru_seq_structs_match_header(cname, py):
+    """The ctypes mirrors of the sequence-GRU argument structs list the header's fields in its order (every
+    field 8 bytes: int64_t or a pointer, so the order fixes the layout)."""
+    txt = open(os.path.join(REPO, "include", "crowdnav.h")).read()
+    body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), txt, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"(\w+)\s*;", body)
+    assert fields == [f for f, _ in py._fields_]
+    assert ctypes.sizeof(py) == 8 * len(fields)
+
+
+def test_gru_seq_rejects_bad_arguments_without_launching(L):
+    assert L.cn_gru_seq_tiles(1) == 1 and L.cn_gru_seq_tiles(128) == 1 and L.cn_gru_seq_tiles(129) == 2
+    segs = (_lib.GruSeqFwd * 3)()
+    assert L.cn_gru_fwd_seq(None, 4, 256, 3, segs) != 0      # at most two GRUs per call
+    assert L.cn_gru_fwd_seq(None, 4, 96 + 4, 1, segs) != 0   # H % 32
+    assert L.cn_gru_fwd_seq(None, 4, 256, 1, segs) != 0      # B = 0, null operands
+    bsegs = (_lib.GruSeqBwd * 1)()
+    assert L.cn_gru_bwd_seq(None, 0, 256, 1, bsegs) != 0     # T = 0
+    assert L.cn_gru_bwd_seq(None, 4, 256, 1, bsegs) != 0
+    assert b"cn_gru_bwd_seq" in L.cn_last_error()
+
+
 def test_config_struct_size_matches(L):
     # a validate call on a deliberately invalid config only reads the struct (no GPU work)
     c = abi.CnConfig()

@@ -192,6 +192,78 @@ def test_masked_gru_kernels_vs_fp64(T, B, F, H):
         np.testing.assert_allclose(a.numpy(), b.numpy(), atol=tol, rtol=0, err_msg=n)
 
 
+def _gru_case(g, T, B, F, H):
+    x = torch.randn(T, B, F, generator=g)
+    h0 = torch.randn(B, H, generator=g) * 0.5
+    masks = (torch.rand(T, B, generator=g) > 0.2).float()
+    masks[:, 0] = 0.0
+    gru = torch.nn.GRU(F, H)
+    ws = [gru.weight_ih_l0.detach(), gru.weight_hh_l0.detach(),
+          torch.randn(3 * H, generator=g) * 0.1, torch.randn(3 * H, generator=g) * 0.1]
+    return x, h0, masks, ws, torch.randn(T, B, H, generator=g), torch.randn(B, H, generator=g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,Bs,F,H", [(9, (300, 45), 64, 256), (3, (1, 129), 64, 128), (17, (2048 * 10, 2048), 64, 256),
+                                      (2, (128, 256), 32, 64)])
+def test_masked_gru_group_vs_fp64(T, Bs, F, H):
+    """ops.masked_gru_group (two GRUs in shared cn_gru_fwd_seq / cn_gru_bwd_seq launches: the spatial and
+    temporal edge RNNs) vs the float64 restatement of each GRU on its own: outputs, final states and every
+    gradient of both. Ragged row tiles on either side of the boundary (1, 129, 45) and C4's minibatch shape
+    (20,480 + 2,048 rows). Tolerances as test_masked_gru_kernels_vs_fp64."""
+    from crowdnav_dsrnn_amd import ops
+
+    g = torch.Generator().manual_seed(T * 7 + Bs[0])
+    cases = [_gru_case(g, T, B, F, H) for B in Bs]
+
+    def run(group, dev, dt):
+        leaves, grus, loss = [], [], 0
+        for x, h0, masks, ws, _, _ in cases:
+            lv = [t.to(dev, dt).requires_grad_(True) for t in (x, h0, *ws)]
+            leaves.append(lv)
+            grus.append((lv[0], lv[1], masks.to(dev, dt), *lv[2:]))
+        res = group(*grus)
+        for (out, hT), (_, _, _, _, dout, dhT) in zip(res, cases):
+            loss = loss + (out * dout.to(dev, dt)).sum() + (hT * dhT.to(dev, dt)).sum()
+        loss.backward()
+        return [[out.detach().cpu().double(), hT.detach().cpu().double()] + [l.grad.cpu().double() for l in lv]
+                for (out, hT), lv in zip(res, leaves)]
+
+    got = run(ops.masked_gru_group, "cuda:0", torch.float32)
+    want = run(lambda *grus: [masked_gru_ref(*gr) for gr in grus], "cpu", torch.float64)
+    names = ["out", "hT", "dx", "dh0", "dW_ih", "dW_hh", "db_ih", "db_hh"]
+    for k in range(2):
+        for n, a, b in zip(names, got[k], want[k]):
+            tol = 2e-5 if n in ("out", "hT") else 1e-4 * max(1.0, float(b.abs().max()))
+            np.testing.assert_allclose(a.numpy(), b.numpy(), atol=tol, rtol=0, err_msg="gru %d %s" % (k, n))
+
+
+@pytest.mark.gpu
+def test_masked_gru_seq_matches_per_step_path():
+    """The native sequence path (cn_gru_fwd_seq / cn_gru_bwd_seq) vs the per-step path it replaced
+    (cn_gru_fwd_fused per step; cn_gru_bwd_step_gates + a library GEMM per step) on the same fp32 operands:
+    the forward runs the same kernel arithmetic (bit-identical outputs); the backward's recurrent GEMM sums
+    in another order (atol 2e-5 x scale)."""
+    from crowdnav_dsrnn_amd import ops
+
+    g = torch.Generator().manual_seed(5)
+    T, B, F, H = 12, 3000, 64, 256
+    x, h0, masks, ws, dout, dhT = _gru_case(g, T, B, F, H)
+
+    def run(fn):
+        lv = [t.cuda().requires_grad_(True) for t in (x, h0, *ws)]
+        out, hT = fn(lv[0], lv[1], masks.cuda(), *lv[2:])
+        ((out * dout.cuda()).sum() + (hT * dhT.cuda()).sum()).backward()
+        return [out.detach(), hT.detach()] + [l.grad for l in lv]
+
+    got = run(ops.masked_gru)
+    ref = run(ops._MaskedGRU.apply)
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+    for n, a, b in zip(["dx", "dh0", "dW_ih", "dW_hh", "db_ih", "db_hh"], got[2:], ref[2:]):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), atol=2e-5 * max(1.0, float(b.abs().max())),
+                                   rtol=0, err_msg=n)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("K,m,n,relu", [(262144, 64, 2, True), (100003, 64, 3, True), (5000, 3, 7, False),
                                         (70001, 2, 256, False), (1, 1, 256, False), (33, 64, 2, True),
@@ -330,3 +402,27 @@ def test_gru_fused_step_vs_gemm_plus_gates(B, H, G):
     for n, a, r in zip(("h_out", "hm_next", "save", "h_out2"), got, ref):
         assert torch.isfinite(a).all(), n
         np.testing.assert_allclose(a.cpu().numpy(), r.cpu().numpy(), atol=2e-6, rtol=0, err_msg=n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("E,A,det", [(4096, 2, False), (37, 2, True), (5, 3, False)])
+def test_gaussian_act_kernel_vs_torch(E, A, det):
+    """cn_gaussian_act (ops.gaussian_act) vs DiagGaussian -> FixedNormal.sample / mode + log_probs in torch
+    on the same N(0, 1) draw (same generator state): action and summed log-probability, float32 (exp / log of
+    the device math library on both sides; atol 2e-6 x scale)."""
+    from crowdnav_dsrnn_amd import ops
+    from crowdnav_dsrnn_amd.policy.distributions import FixedNormal
+
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(E + A)
+    mean = torch.randn((E, A), generator=g, device="cuda:0")
+    logstd = torch.randn((A,), generator=g, device="cuda:0") * 0.5
+    torch.manual_seed(11)
+    act, lp = ops.gaussian_act(mean, logstd, det)
+    torch.manual_seed(11)
+    d = FixedNormal(mean, (torch.zeros_like(mean) + logstd.view(1, -1)).exp())
+    ref = d.mode() if det else d.sample()
+    ref_lp = d.log_probs(ref)
+    np.testing.assert_allclose(act.cpu().numpy(), ref.cpu().numpy(), atol=2e-6 * max(1.0, float(ref.abs().max())), rtol=0)
+    np.testing.assert_allclose(lp.cpu().numpy(), ref_lp.cpu().numpy(), atol=2e-6 * max(1.0, float(ref_lp.abs().max())),
+                               rtol=0)
