@@ -359,16 +359,21 @@ def run_c4(args, torch, dist, device, rank, world):
     roof = gru_gemm_roofline(torch, device, E // c.ppo.num_mini_batch * N, 256) if rank == 0 else None
     if rank == 0 and timing:
         # the roofline of record: the same kernel timed IN the loop (all its launches of the timed updates)
-        n_launch = sum(T for (_, _, T, _, _) in timing)
-        secs = sum(e0.elapsed_time(e1) for (_, _, _, e0, e1) in timing) / 1e3
-        B0, H0 = timing[0][0], timing[0][1]
-        flop = 2.0 * B0 * H0 * 3 * H0
+        n_launch = sum(t[2] for t in timing)
+        secs = sum(t[3].elapsed_time(t[4]) for t in timing) / 1e3
+        B0, H0, F0 = timing[0][0], timing[0][1], timing[0][5]
+        flop = 2.0 * B0 * (H0 + F0) * 3 * H0   # recurrent GEMM + the in-kernel input projection (F0 > 0)
         iso = roof
         tf = flop * n_launch / secs / 1e12
         roof = dict(iso, achieved=round(tf, 3), frac=round(tf / FP32_MFMA_PEAK_TFLOPS, 4),
                     avg_launch_us=round(secs / n_launch * 1e6, 2), launches_timed=n_launch,
+                    kernel="edge-RNN fused step of the PPO forward (cn_gru_fwd_seq: the spatial and temporal edge GRUs, "
+                           "%d rows per launch; x W_ih^T (F = %d) + hm W_hh^T + b on the fp32 MFMA, gates in the "
+                           "epilogue)" % (B0, F0),
+                    flop_per_launch=flop,
                     method="HIP events around every training forward's fused-step loop, on its stream, inside "
                            "the timed updates",
+                    isolated_kernel=iso["kernel"], isolated_flop_per_launch=iso["flop_per_launch"],
                     isolated_avg_launch_us=iso["avg_launch_us"])
     if rank == 0:
         steps_per_update = c.ppo.num_steps * E

@@ -18,14 +18,23 @@ class GruSeqFwd(ctypes.Structure):
     """cn_gru_seq_fwd (include/crowdnav.h): one GRU of a cn_gru_fwd_seq call (device pointers)."""
     _fields_ = [("B", ctypes.c_int64), ("gi", ctypes.c_void_p), ("w_hh", ctypes.c_void_p), ("b_hh", ctypes.c_void_p),
                 ("m", ctypes.c_void_p), ("out", ctypes.c_void_p), ("hm", ctypes.c_void_p), ("save", ctypes.c_void_p),
-                ("nh", ctypes.c_int64)]
+                ("nh", ctypes.c_int64), ("x", ctypes.c_void_p), ("w_ih", ctypes.c_void_p), ("b_ih", ctypes.c_void_p),
+                ("F", ctypes.c_int64)]
 
 
 class GruSeqBwd(ctypes.Structure):
     """cn_gru_seq_bwd (include/crowdnav.h): one GRU of a cn_gru_bwd_seq call (device pointers)."""
     _fields_ = [("B", ctypes.c_int64), ("w_hh_t", ctypes.c_void_p), ("m", ctypes.c_void_p), ("dout", ctypes.c_void_p),
                 ("save", ctypes.c_void_p), ("hm", ctypes.c_void_p), ("acc", ctypes.c_void_p), ("g", ctypes.c_void_p),
-                ("part", ctypes.c_void_p)]
+                ("db_ih", ctypes.c_void_p), ("db_hh", ctypes.c_void_p)]
+
+
+class GruStepSeg(ctypes.Structure):
+    """cn_gru_step_seg (include/crowdnav.h): one GRU of a cn_gru_fwd_step_group call (device pointers)."""
+    _fields_ = [("B", ctypes.c_int64), ("gi", ctypes.c_void_p), ("x", ctypes.c_void_p), ("w_ih", ctypes.c_void_p),
+                ("b_ih", ctypes.c_void_p), ("F", ctypes.c_int64), ("hm", ctypes.c_void_p), ("w_hh", ctypes.c_void_p),
+                ("b_hh", ctypes.c_void_p), ("h_out", ctypes.c_void_p), ("h_out2", ctypes.c_void_p),
+                ("g2", ctypes.c_int64), ("ld2", ctypes.c_int64)]
 
 
 class NativeLibraryMissing(RuntimeError):
@@ -118,11 +127,13 @@ def lib():
         L.cn_gru_bias_reduce.restype = i32
         L.cn_gaussian_act.argtypes = [vp, i64, ctypes.c_int] + [vp] * 5
         L.cn_gaussian_act.restype = i32
-        L.cn_gru_seq_tiles.argtypes = [i64]
-        L.cn_gru_seq_tiles.restype = i64
+        L.cn_gru_bwd_seq_work_elems.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqBwd)]
+        L.cn_gru_bwd_seq_work_elems.restype = i64
+        L.cn_gru_fwd_step_group.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruStepSeg)]
+        L.cn_gru_fwd_step_group.restype = i32
         L.cn_gru_fwd_seq.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqFwd)]
         L.cn_gru_fwd_seq.restype = i32
-        L.cn_gru_bwd_seq.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqBwd)]
+        L.cn_gru_bwd_seq.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqBwd), vp]
         L.cn_gru_bwd_seq.restype = i32
         L.cn_set_graph_mode.argtypes = [vp, vp, ctypes.c_int]
         L.cn_wgrad_work_elems.argtypes = [i64, ctypes.c_int, ctypes.c_int]
@@ -158,7 +169,7 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_spatial_attn_fwd",
             "cn_spatial_attn_bwd", "cn_wgrad_work_elems", "cn_wgrad",
             "cn_gru_bias_blocks", "cn_gru_bwd_step_bias", "cn_gru_bwd_step_gates", "cn_gru_bias_work_elems", "cn_gru_bias_reduce",
-            "cn_gru_seq_tiles", "cn_gru_fwd_seq", "cn_gru_bwd_seq", "cn_gaussian_act",
+            "cn_gru_bwd_seq_work_elems", "cn_gru_fwd_step_group", "cn_gru_fwd_seq", "cn_gru_bwd_seq", "cn_gaussian_act",
             "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad",
             "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict",
             "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"]

@@ -263,11 +263,19 @@ struct GfSeg {
     const float *gi, *hm, *w_hh, *b_hh, *m_next;
     float *h_out, *hm_next, *save, *h_out2;
     int64_t g2, ld2;
+    // input projection in the kernel (template XM): gi = x W_ih^T + b_ih from x [B][F], w_ih [3H][F], b_ih [3H]
+    const float *x, *w_ih, *b_ih;
+    int64_t F;
 };
 struct GfArgs {
     GfSeg s0, s1;
     int rt0, rt_total, unit_tiles, H;
 };
+// XM (input projection in the kernel): the K loop first runs the F / 32 chunks of x against W_ih (r and z into
+// the same accumulators as their recurrent parts, n into a fourth one: gi_n stays separate from gh_n), then
+// the H / 32 chunks of hm against W_hh; the epilogue adds b_ih and b_hh. gi ([B][3H], 3 of the 10 floats the
+// step moves per output, and its T * B * 3H buffer) is never materialised.
+template <bool XM>
 __global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(const GfArgs P)
 {
     // LDS: one A / B chunk buffer during the K loop, then the three gate accumulators of the tile
@@ -330,7 +338,7 @@ __global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(const GfArgs P)
         *(float4 *)(db + 2 * GF_BU * GF_LD) = rb2;                                        \
     }
     const int li = lane & 31, p4 = (lane >> 5) * 4;
-#define GF_MMA(buf)                                                                                          \
+#define GF_MMA(buf, A2)                                                                                      \
     {                                                                                                        \
         const float *a_base = sA0 + (buf) * SA + (wave * 32 + li) * GF_LD + p4;                              \
         const float *b_base = sB0 + (buf) * SB + li * GF_LD + p4;                                            \
@@ -339,54 +347,119 @@ __global__ __launch_bounds__(256, 3) void cn_gru_fused_kernel(const GfArgs P)
             const float4 a = *(const float4 *)(a_base + 8 * c);                                              \
             float4 bv[3];                                                                                    \
             _Pragma("unroll") for (int g = 0; g < 3; ++g) bv[g] = *(const float4 *)(b_base + g * GF_BU * GF_LD + 8 * c); \
-            _Pragma("unroll") for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bv[g].x, acc[g], 0, 0, 0); \
-            _Pragma("unroll") for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bv[g].y, acc[g], 0, 0, 0); \
-            _Pragma("unroll") for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bv[g].z, acc[g], 0, 0, 0); \
-            _Pragma("unroll") for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bv[g].w, acc[g], 0, 0, 0); \
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bv[0].x, acc[0], 0, 0, 0);                   \
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bv[1].x, acc[1], 0, 0, 0);                   \
+            A2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, bv[2].x, A2, 0, 0, 0);                           \
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bv[0].y, acc[0], 0, 0, 0);                   \
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bv[1].y, acc[1], 0, 0, 0);                   \
+            A2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, bv[2].y, A2, 0, 0, 0);                           \
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bv[0].z, acc[0], 0, 0, 0);                   \
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bv[1].z, acc[1], 0, 0, 0);                   \
+            A2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, bv[2].z, A2, 0, 0, 0);                           \
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bv[0].w, acc[0], 0, 0, 0);                   \
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bv[1].w, acc[1], 0, 0, 0);                   \
+            A2 = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, bv[2].w, A2, 0, 0, 0);                           \
         }                                                                                                    \
     }
 
-    gf_f32x16 acc[3];
+    gf_f32x16 acc[3], acc_in;
 #pragma unroll
     for (int g = 0; g < 3; ++g)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[g][e] = 0.0f;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc_in[e] = 0.0f;
 
     const int nch = H / GF_KC;
     float4 eg[4][3], eh[4];
 #define GF_EPI_LOAD()                                                                    \
     _Pragma("unroll") for (int i = 0; i < 4; ++i)                                       \
     {                                                                                    \
-        const float *gib = gi + ar[i] * 3 * H + u0 + lc;                                 \
-        _Pragma("unroll") for (int g = 0; g < 3; ++g) eg[i][g] = *(const float4 *)(gib + g * H); \
+        if (!XM) {                                                                       \
+            const float *gib = gi + ar[i] * 3 * H + u0 + lc;                             \
+            _Pragma("unroll") for (int g = 0; g < 3; ++g) eg[i][g] = *(const float4 *)(gib + g * H); \
+        }                                                                                \
         eh[i] = *(const float4 *)(hm + ar[i] * H + u0 + lc);                             \
     }
-    GF_GLOAD(0)
-    GF_LSTORE(0)
-    __syncthreads();
+    if (XM) {
+        // x chunks first (A = x rows, B = W_ih rows; n into acc_in), then the recurrent ones. Two loops, and
+        // the x addresses formed per load, so no second address set stays live across the recurrent chunks.
+        const int64_t F = S.F;
+        const int ncx = (int)(F / GF_KC);
+        const float *__restrict__ xx = S.x, *__restrict__ wih = S.w_ih;
+#define GF_GLOAD_X(kc)                                                                        \
+    {                                                                                         \
+        ra0 = *(const float4 *)(xx + ar[0] * F + lc + (kc));                                  \
+        ra1 = *(const float4 *)(xx + ar[1] * F + lc + (kc));                                  \
+        ra2 = *(const float4 *)(xx + ar[2] * F + lc + (kc));                                  \
+        ra3 = *(const float4 *)(xx + ar[3] * F + lc + (kc));                                  \
+        const float *xb = wih + (int64_t)(u0 + lr) * F + lc + (kc);                           \
+        rb0 = *(const float4 *)(xb);                                                          \
+        rb1 = *(const float4 *)(xb + (int64_t)H * F);                                         \
+        rb2 = *(const float4 *)(xb + (int64_t)2 * H * F);                                     \
+    }
+        GF_GLOAD_X(0)
+        GF_LSTORE(0)
+        __syncthreads();
+        for (int ch = 0; ch < ncx; ++ch) {
+            if (ch + 1 < ncx) {
+                GF_GLOAD_X((ch + 1) * GF_KC)
+            } else {
+                GF_GLOAD(0)   // the first recurrent chunk
+            }
+            GF_MMA(0, acc_in)
+            __syncthreads();
+            GF_LSTORE(0)
+            __syncthreads();
+        }
+#undef GF_GLOAD_X
+    } else {
+        GF_GLOAD(0)
+        GF_LSTORE(0)
+        __syncthreads();
+    }
     for (int ch = 0; ch + 1 < nch; ++ch) {
         GF_GLOAD((ch + 1) * GF_KC)  // in flight during this chunk's MFMAs
-        GF_MMA(0)
+        GF_MMA(0, acc[2])
         __syncthreads();
         GF_LSTORE(0)
         __syncthreads();
     }
-    // last chunk: the epilogue's operands (gi's three gate blocks and hm of this thread's 4 x 4 outputs) are
-    // fetched while its MFMAs run
+    // last chunk (a recurrent one): the epilogue's operands (gi's three gate blocks unless XM, and hm of this
+    // thread's 4 x 4 outputs) are fetched while its MFMAs run
     GF_EPI_LOAD()
 #undef GF_EPI_LOAD
-    GF_MMA(0)
+    GF_MMA(0, acc[2])
     __syncthreads();  // every wave is done reading the chunk buffers before sC overwrites them
 #undef GF_GLOAD
 #undef GF_LSTORE
 #undef GF_MMA
 
-    // accumulators -> LDS: lane holds unit li of rows (e & 3) + 8 (e >> 2) + 4 (lane >> 5) of its wave's 32
+    // accumulators -> LDS: lane holds unit li of rows (e & 3) + 8 (e >> 2) + 4 (lane >> 5) of its wave's 32.
+    // XM: the input part of n (acc_in) goes through region 2 first; gi_r / gi_z are b_ih alone (their x parts
+    // are in acc r / z) and gi_n = acc_in + b_ih_n
+#define GF_TO_LDS(g, A)                                                                                        \
+    _Pragma("unroll") for (int e = 0; e < 16; ++e)                                                           \
+        smem[((g) * GF_BM + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * LDC + li] = (A)[e];
+    GF_TO_LDS(0, acc[0])
+    GF_TO_LDS(1, acc[1])
+    if (XM) {
+        GF_TO_LDS(2, acc_in)
+        __syncthreads();
+        const float *b_ih = S.b_ih;
+        const float4 bir = *(const float4 *)(b_ih + u0 + lc), biz = *(const float4 *)(b_ih + H + u0 + lc),
+                     bin = *(const float4 *)(b_ih + 2 * H + u0 + lc);
 #pragma unroll
-    for (int g = 0; g < 3; ++g)
-#pragma unroll
-        for (int e = 0; e < 16; ++e)
-            smem[(g * GF_BM + wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * LDC + li] = acc[g][e];
+        for (int i = 0; i < 4; ++i) {
+            const float *pc = smem + (2 * GF_BM + lr + 32 * i) * LDC + lc;
+            eg[i][0] = bir;
+            eg[i][1] = biz;
+            eg[i][2] = make_float4(pc[0] + bin.x, pc[1] + bin.y, pc[2] + bin.z, pc[3] + bin.w);
+        }
+        __syncthreads();
+    }
+    GF_TO_LDS(2, acc[2])
+#undef GF_TO_LDS
     __syncthreads();
 
     const float4 br = *(const float4 *)(b_hh + u0 + lc), bz = *(const float4 *)(b_hh + H + u0 + lc),
@@ -654,9 +727,292 @@ __global__ __launch_bounds__(256) void cn_gaussian_act_kernel(int64_t E, int A, 
     logp[e] = lp;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Split-K variants for launches with few rows (the DSRNN node GRU: 2,048 x 128 per PPO minibatch, the
+// rollout's 4,096-row node step): with 128-row tiles such a launch has fewer workgroups than CUs and each
+// wave runs the whole K chain (node GRU: 16 row tiles x 4 unit tiles = 64 workgroups, 5 us of MFMA per
+// wave). Here a workgroup owns 32 rows x 32 hidden units and its 4 waves split K (wave w takes K chunks
+// w, w + 4, ...), loading their MFMA operands straight from global memory into registers in the
+// instruction's layout (lane (i, p) holds row / unit i at k = 8q + 4p .. + 3 of chunk q: no LDS staging);
+// the 4 partial tiles are summed through LDS in wave order (deterministic), then the same epilogue
+// arithmetic as the 128-row kernels runs with one output row x 4 units per thread.
+// ------------------------------------------------------------------------------------------------
+constexpr int SK_BM = 32;
+
+template <bool XM>
+__global__ __launch_bounds__(256) void cn_gru_fused_sk_kernel(const GfArgs P)
+{
+    __shared__ float sP[4][XM ? 4 : 3][SK_BM][33];
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, k = bid >> 3;
+    const int unit_tiles = P.unit_tiles, H = P.H;
+    const int ut = k % unit_tiles;
+    int rt = (k / unit_tiles) * 8 + xcd;
+    if (rt >= P.rt_total) return;  // grid padding (whole workgroup, before any barrier)
+    const bool second = rt >= P.rt0;
+    const GfSeg S = second ? P.s1 : P.s0;
+    if (second) rt -= P.rt0;
+    const int64_t B = S.B;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 31, p4 = (lane >> 5) * 4;
+    const int64_t row0 = (int64_t)rt * SK_BM;
+    const int u0 = ut * GF_BU;
+    // epilogue map: thread -> row er, units u0 + lc .. + 3; its operands are requested first
+    const int er = tid >> 3, lc = (tid & 7) * 4;
+    const int64_t eb = min(row0 + er, B - 1);
+    float4 eg[3];
+    if (!XM) {
+#pragma unroll
+        for (int g = 0; g < 3; ++g) eg[g] = *(const float4 *)(S.gi + eb * 3 * H + g * H + u0 + lc);
+    }
+    const float4 hp = *(const float4 *)(S.hm + eb * H + u0 + lc);
+
+    // XM: chunks 0 .. F/32 - 1 are x against W_ih (n into acc[3]), then hm against W_hh
+    gf_f32x16 acc[XM ? 4 : 3];
+#pragma unroll
+    for (int g = 0; g < (XM ? 4 : 3); ++g)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[g][e] = 0.0f;
+    const float *pa = S.hm + min(row0 + li, B - 1) * H + p4;
+    const float *pb = S.w_hh + (int64_t)(u0 + li) * H + p4;
+    const int64_t b_step = (int64_t)H * H;
+    const int nch = H / GF_KC;
+    const int64_t F = XM ? S.F : 0;
+    const int ncx = (int)(F / GF_KC);
+    const float *xa = XM ? S.x + min(row0 + li, B - 1) * F + p4 : nullptr;
+    const float *xb = XM ? S.w_ih + (int64_t)(u0 + li) * F + p4 : nullptr;
+    for (int c = wave; c < ncx + nch; c += 4) {
+        const bool isx = c < ncx;
+        const float *ap = isx ? xa + c * GF_KC : pa + (c - ncx) * GF_KC;
+        const float *bp = isx ? xb + c * GF_KC : pb + (c - ncx) * GF_KC;
+        const int64_t bs = isx ? (int64_t)H * F : b_step;
+        float4 a[4], b[3][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) a[q] = *(const float4 *)(ap + 8 * q);
+#pragma unroll
+        for (int g = 0; g < 3; ++g)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b[g][q] = *(const float4 *)(bp + g * bs + 8 * q);
+        if (XM && isx) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b[0][q].x, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b[1][q].x, acc[1], 0, 0, 0);
+                acc[XM ? 3 : 2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b[2][q].x, acc[XM ? 3 : 2], 0, 0, 0);
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, b[0][q].y, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, b[1][q].y, acc[1], 0, 0, 0);
+                acc[XM ? 3 : 2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, b[2][q].y, acc[XM ? 3 : 2], 0, 0, 0);
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, b[0][q].z, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, b[1][q].z, acc[1], 0, 0, 0);
+                acc[XM ? 3 : 2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, b[2][q].z, acc[XM ? 3 : 2], 0, 0, 0);
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, b[0][q].w, acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, b[1][q].w, acc[1], 0, 0, 0);
+                acc[XM ? 3 : 2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, b[2][q].w, acc[XM ? 3 : 2], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+#pragma unroll
+                for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, b[g][q].x, acc[g], 0, 0, 0);
+#pragma unroll
+                for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, b[g][q].y, acc[g], 0, 0, 0);
+#pragma unroll
+                for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, b[g][q].z, acc[g], 0, 0, 0);
+#pragma unroll
+                for (int g = 0; g < 3; ++g) acc[g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, b[g][q].w, acc[g], 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < (XM ? 4 : 3); ++g)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sP[wave][g][(e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)][li] = acc[g][e];
+    __syncthreads();
+    const int64_t b = row0 + er;
+    if (b >= B) return;
+    float cs[3][4];
+#pragma unroll
+    for (int g = 0; g < 3; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            cs[g][j] = ((sP[0][g][er][lc + j] + sP[1][g][er][lc + j]) + sP[2][g][er][lc + j]) + sP[3][g][er][lc + j];
+    const float4 cr = make_float4(cs[0][0], cs[0][1], cs[0][2], cs[0][3]);
+    const float4 cz = make_float4(cs[1][0], cs[1][1], cs[1][2], cs[1][3]);
+    const float4 cn = make_float4(cs[2][0], cs[2][1], cs[2][2], cs[2][3]);
+    const float *b_hh = S.b_hh;
+    const float4 br = *(const float4 *)(b_hh + u0 + lc), bz = *(const float4 *)(b_hh + H + u0 + lc),
+                 bn = *(const float4 *)(b_hh + 2 * H + u0 + lc);
+    if (XM) {
+        const float *b_ih = S.b_ih;
+        float ci[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ci[j] = ((sP[0][XM ? 3 : 0][er][lc + j] + sP[1][XM ? 3 : 0][er][lc + j]) +
+                                             sP[2][XM ? 3 : 0][er][lc + j]) + sP[3][XM ? 3 : 0][er][lc + j];
+        const float4 bin = *(const float4 *)(b_ih + 2 * H + u0 + lc);
+        eg[0] = *(const float4 *)(b_ih + u0 + lc);
+        eg[1] = *(const float4 *)(b_ih + H + u0 + lc);
+        eg[2] = make_float4(ci[0] + bin.x, ci[1] + bin.y, ci[2] + bin.z, ci[3] + bin.w);
+    }
+    const float4 ir = eg[0], iz = eg[1], in = eg[2];
+    float4 hr, hz, hn, r, z, n, h;
+#define CN_GATE(c)                                 \
+    hr.c = cr.c + br.c;                            \
+    hz.c = cz.c + bz.c;                            \
+    hn.c = cn.c + bn.c;                            \
+    r.c = sigm(hr.c + ir.c);                       \
+    z.c = sigm(hz.c + iz.c);                       \
+    n.c = tanhf(in.c + hn.c * r.c);                \
+    h.c = (hp.c - n.c) * z.c + n.c;
+    CN_GATE(x) CN_GATE(y) CN_GATE(z) CN_GATE(w)
+#undef CN_GATE
+    const int64_t o = b * H + u0 + lc;
+    *(float4 *)(S.h_out + o) = h;
+    if (S.h_out2) {
+        float *d = S.h_out2 + (b / S.g2) * S.ld2 + (b % S.g2) * H + u0 + lc;
+        d[0] = h.x;
+        d[1] = h.y;
+        d[2] = h.z;
+        d[3] = h.w;
+    }
+    if (S.hm_next) {
+        const float m = S.m_next ? S.m_next[b] : 1.0f;
+        *(float4 *)(S.hm_next + o) = make_float4(h.x * m, h.y * m, h.z * m, h.w * m);
+    }
+    if (S.save) {
+        float *sv = S.save + b * 4 * H + u0 + lc;
+        *(float4 *)(sv) = r;
+        *(float4 *)(sv + H) = z;
+        *(float4 *)(sv + 2 * H) = n;
+        *(float4 *)(sv + 3 * H) = hn;
+    }
+}
+
+__global__ __launch_bounds__(256) void cn_gru_bwd_sk_kernel(const GbArgs P)
+{
+    __shared__ float sP[4][SK_BM][33];
+    __shared__ float red[256 * 16];
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, k = bid >> 3;
+    const int unit_tiles = P.unit_tiles, H = P.H;
+    const int ut = k % unit_tiles;
+    int rt = (k / unit_tiles) * 8 + xcd;
+    if (rt >= P.rt_total) return;  // grid padding (whole workgroup, before any barrier)
+    const bool second = rt >= P.rt0;
+    const GbSeg S = second ? P.s1 : P.s0;
+    if (second) rt -= P.rt0;
+    const int64_t B = S.B;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int li = lane & 31, p4 = (lane >> 5) * 4;
+    const int64_t row0 = (int64_t)rt * SK_BM;
+    const int u0 = ut * GF_BU;
+    const int er = tid >> 3, lc = (tid & 7) * 4;
+    const int64_t eb = min(row0 + er, B - 1);
+    const bool gates = S.g != nullptr;
+    const int64_t eo = eb * H + u0 + lc;
+    // epilogue operands first (they do not depend on the GEMM)
+    const float4 ai = *(const float4 *)(S.a + eo);
+    float4 es[4], d = make_float4(0.f, 0.f, 0.f, 0.f), hp = d;
+    float m = 1.0f;
+    if (gates) {
+        const float *sv = S.save + eb * 4 * H + u0 + lc;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) es[q] = *(const float4 *)(sv + q * H);
+        hp = *(const float4 *)(S.hm + eo);
+        if (S.dout) d = *(const float4 *)(S.dout + eo);
+        if (S.m_next) m = S.m_next[eb];
+    }
+    gf_f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+    if (S.gk) {
+        const int K3 = 3 * H;
+        const float *pa = S.gk + min(row0 + li, B - 1) * 4 * H + H + p4;
+        const float *pb = S.wt + (int64_t)(u0 + li) * K3 + p4;
+        const int nch = K3 / GF_KC;
+        for (int c = wave; c < nch; c += 4) {
+            const int kc = c * GF_KC;
+            float4 a[4], bv[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                a[q] = *(const float4 *)(pa + kc + 8 * q);
+                bv[q] = *(const float4 *)(pb + kc + 8 * q);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].x, bv[q].x, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].y, bv[q].y, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].z, bv[q].z, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[q].w, bv[q].w, acc, 0, 0, 0);
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < 16; ++e) sP[wave][(e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)][li] = acc[e];
+    __syncthreads();
+    const int64_t b = row0 + er;
+    const bool live = b < B;
+    float4 sr = make_float4(0.f, 0.f, 0.f, 0.f), sz = sr, sn = sr, shn = sr;
+    if (live) {
+        float cs[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cs[j] = ((sP[0][er][lc + j] + sP[1][er][lc + j]) + sP[2][er][lc + j]) + sP[3][er][lc + j];
+        const float4 v = make_float4(cs[0] + ai.x, cs[1] + ai.y, cs[2] + ai.z, cs[3] + ai.w);
+        const int64_t o = b * H + u0 + lc;
+        if (!gates) {
+            *(float4 *)(S.a + o) = v;
+        } else {
+            const float4 r = es[0], z = es[1], n = es[2], hn = es[3];
+            float4 a, dr, dz, dn, dhn;
+#define CN_GBWD(c)                                                  \
+    {                                                               \
+        const float gc = v.c * m + d.c;                             \
+        const float dnc = gc * (1.0f - z.c) * (1.0f - n.c * n.c);   \
+        const float dzc = gc * (hp.c - n.c) * z.c * (1.0f - z.c);   \
+        const float drc = dnc * hn.c * r.c * (1.0f - r.c);          \
+        a.c = gc * z.c;                                             \
+        dr.c = drc;                                                 \
+        dz.c = dzc;                                                 \
+        dn.c = dnc;                                                 \
+        dhn.c = dnc * r.c;                                          \
+        sr.c = drc; sz.c = dzc; sn.c = dnc; shn.c = dhn.c;          \
+    }
+            CN_GBWD(x) CN_GBWD(y) CN_GBWD(z) CN_GBWD(w)
+#undef CN_GBWD
+            *(float4 *)(S.a + o) = a;
+            float *gr = S.g + b * 4 * H + u0 + lc;
+            *(float4 *)(gr) = dn;
+            *(float4 *)(gr + H) = dr;
+            *(float4 *)(gr + 2 * H) = dz;
+            *(float4 *)(gr + 3 * H) = dhn;
+        }
+    }
+    if (!gates) return;
+    // column sums of the tile (32 units x 4 gates) over its 32 rows, in row order through LDS
+    float *rw = red + tid * 16;
+    *(float4 *)(rw) = sr;
+    *(float4 *)(rw + 4) = sz;
+    *(float4 *)(rw + 8) = sn;
+    *(float4 *)(rw + 12) = shn;
+    __syncthreads();
+    if (tid >= 4 * GF_BU) return;
+    const int q = tid / GF_BU, cu = tid - q * GF_BU;
+    const float *src = red + (cu >> 2) * 16 + q * 4 + (cu & 3);
+    float s = 0.0f;
+    for (int r = 0; r < SK_BM; ++r) s += src[r * 8 * 16];
+    S.part[(int64_t)rt * 4 * H + q * H + u0 + cu] = s;
+}
+
+// 128-row tiles unless that leaves fewer workgroups than CUs (then the split-K kernels, 32-row tiles)
+static inline bool use_split_k(int64_t rows, int H)
+{
+    return (rows + GF_BM - 1) / GF_BM * (H / GF_BU) < 256;
+}
+static inline int64_t row_tile(int64_t rows_total, int H) { return use_split_k(rows_total, H) ? SK_BM : GF_BM; }
+
 static int launch_fwd_fused(hipStream_t st, GfArgs &P, int64_t B0, int64_t B1, int H)
 {
-    const int64_t rt0 = (B0 + GF_BM - 1) / GF_BM, rt1 = (B1 + GF_BM - 1) / GF_BM;
+    const int64_t bm = row_tile(B0 + B1, H);
+    const int64_t rt0 = (B0 + bm - 1) / bm, rt1 = (B1 + bm - 1) / bm;
     const int ut = H / GF_BU;
     const int64_t grid = (rt0 + rt1 + 7) / 8 * 8 * ut;
     if (grid > 0x7fffffff) return cn_set_error(CN_EINVAL, "fused GRU step: B too large");
@@ -665,7 +1021,18 @@ static int launch_fwd_fused(hipStream_t st, GfArgs &P, int64_t B0, int64_t B1, i
     P.unit_tiles = ut;
     P.H = H;
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
-    hipLaunchKernelGGL(cn_gru_fused_kernel, dim3((unsigned)grid), dim3(256), 0, st, P);
+    const bool xm = P.s0.x != nullptr;
+    if (bm == SK_BM) {
+        if (xm)
+            hipLaunchKernelGGL(cn_gru_fused_sk_kernel<true>, dim3((unsigned)grid), dim3(256), 0, st, P);
+        else
+            hipLaunchKernelGGL(cn_gru_fused_sk_kernel<false>, dim3((unsigned)grid), dim3(256), 0, st, P);
+    } else {
+        if (xm)
+            hipLaunchKernelGGL(cn_gru_fused_kernel<true>, dim3((unsigned)grid), dim3(256), 0, st, P);
+        else
+            hipLaunchKernelGGL(cn_gru_fused_kernel<false>, dim3((unsigned)grid), dim3(256), 0, st, P);
+    }
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }
@@ -710,7 +1077,8 @@ int cn_gru_fwd_fused(void *stream, int64_t B, int H, const float *gi, const floa
     if (h_out2 && (g2 <= 0 || ld2 < g2 * H))
         return cn_set_error(CN_EINVAL, "cn_gru_fwd_fused: g2 > 0 and ld2 >= g2 * H required");
     GfArgs P{};
-    P.s0 = GfSeg{B, gi, hm, w_hh, b_hh, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2};
+    P.s0 = GfSeg{B, gi, hm, w_hh, b_hh, m_next, h_out, hm_next, save, h_out2, h_out2 ? g2 : (int64_t)1, ld2,
+                 nullptr, nullptr, nullptr, 0};
     P.s1 = P.s0;
     return launch_fwd_fused((hipStream_t)stream, P, B, 0, H);
 }
@@ -727,13 +1095,36 @@ int cn_gaussian_act(void *stream, int64_t E, int A, const float *mean, const flo
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }
 
-int64_t cn_gru_seq_tiles(int64_t B) { return (B + GF_BM - 1) / GF_BM; }
-
 static bool aligned16(std::initializer_list<const void *> ps)
 {
     for (const void *p : ps)
         if ((uintptr_t)p & 15) return false;
     return true;
+}
+
+int cn_gru_fwd_step_group(void *stream, int H, int nseg, const cn_gru_step_seg *segs)
+{
+    if (H <= 0 || H % GF_BU || nseg < 1 || nseg > 2 || !segs)
+        return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_group: H % 32 == 0 and 1 <= nseg <= 2 required");
+    GfArgs P{};
+    for (int s = 0; s < nseg; ++s) {
+        const cn_gru_step_seg &q = segs[s];
+        if (q.B <= 0 || !q.hm || !q.w_hh || !q.b_hh || !q.h_out)
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_group: B > 0 and hm, w_hh, b_hh, h_out required");
+        if ((q.x != nullptr) != (segs[0].x != nullptr))
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_group: every GRU of a call passes gi, or every GRU x");
+        if (q.x ? (!q.w_ih || !q.b_ih || q.F <= 0 || q.F % GF_KC) : !q.gi)
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_group: gi, or x with w_ih, b_ih and F % 32 == 0, required");
+        if (!aligned16({q.gi, q.x, q.w_ih, q.b_ih, q.hm, q.w_hh, q.b_hh, q.h_out}))
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_group: every array must be 16-byte aligned");
+        if (q.h_out2 && (q.g2 <= 0 || q.ld2 < q.g2 * H))
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_step_group: g2 > 0 and ld2 >= g2 * H required");
+        GfSeg g{q.B, q.gi, q.hm, q.w_hh, q.b_hh, nullptr, q.h_out, nullptr, nullptr, q.h_out2,
+                q.h_out2 ? q.g2 : (int64_t)1, q.ld2, q.x, q.w_ih, q.b_ih, q.F};
+        (s ? P.s1 : P.s0) = g;
+    }
+    if (nseg == 1) P.s1 = P.s0;
+    return launch_fwd_fused((hipStream_t)stream, P, segs[0].B, nseg > 1 ? segs[1].B : 0, H);
 }
 
 int cn_gru_fwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_fwd *segs)
@@ -743,9 +1134,13 @@ int cn_gru_fwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_fwd *s
     for (int s = 0; s < nseg; ++s) {
         const cn_gru_seq_fwd &q = segs[s];
         if (q.B <= 0 || q.nh < 1 || q.nh > T) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: B > 0 and 1 <= nh <= T required");
-        if (!q.gi || !q.w_hh || !q.b_hh || !q.m || !q.out || !q.hm) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: null operand");
-        if (!aligned16({q.gi, q.w_hh, q.b_hh, q.out, q.hm, q.save}))
-            return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: gi, w_hh, b_hh, out, hm and save must be 16-byte aligned");
+        if (!q.w_hh || !q.b_hh || !q.m || !q.out || !q.hm) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: null operand");
+        if ((q.x != nullptr) != (segs[0].x != nullptr))
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: every GRU of a call passes gi, or every GRU x / w_ih / b_ih");
+        if (q.x ? (!q.w_ih || !q.b_ih || q.F <= 0 || q.F % GF_KC) : !q.gi)
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: gi, or x with w_ih, b_ih and F % 32 == 0, required");
+        if (!aligned16({q.gi, q.w_hh, q.b_hh, q.out, q.hm, q.save, q.x, q.w_ih, q.b_ih}))
+            return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: every array must be 16-byte aligned");
     }
     const int64_t B1 = nseg > 1 ? segs[1].B : 0;
     for (int t = 0; t < T; ++t) {
@@ -754,10 +1149,11 @@ int cn_gru_fwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_fwd *s
             const cn_gru_seq_fwd &q = segs[s];
             const bool last = t + 1 == T;
             const int64_t BH = q.B * H;
-            GfSeg g{q.B, q.gi + t * 3 * BH, q.hm + (t % q.nh) * BH, q.w_hh, q.b_hh,
+            GfSeg g{q.B, q.gi ? q.gi + t * 3 * BH : nullptr, q.hm + (t % q.nh) * BH, q.w_hh, q.b_hh,
                     last ? nullptr : q.m + (t + 1) * q.B, q.out + t * BH,
                     last ? nullptr : q.hm + ((t + 1) % q.nh) * BH, q.save ? q.save + t * 4 * BH : nullptr, nullptr,
-                    1, 0};
+                    1, 0,
+                    q.x ? q.x + t * q.B * q.F : nullptr, q.w_ih, q.b_ih, q.F};
             (s ? P.s1 : P.s0) = g;
         }
         if (nseg == 1) P.s1 = P.s0;
@@ -767,22 +1163,39 @@ int cn_gru_fwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_fwd *s
     return CN_OK;
 }
 
-int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs)
+// workspace of cn_gru_bwd_seq: per GRU the bias partials [T][row tiles][4H], then cn_gru_bias_reduce's work
+static int64_t bwd_part_rows(int64_t B, int64_t bm) { return (B + bm - 1) / bm; }
+
+int64_t cn_gru_bwd_seq_work_elems(int T, int H, int nseg, const cn_gru_seq_bwd *segs)
+{
+    if (T <= 0 || H <= 0 || nseg < 1 || nseg > 2 || !segs) return 0;
+    const int64_t rows = segs[0].B + (nseg > 1 ? segs[1].B : 0);
+    const int64_t bm = row_tile(rows, H);
+    int64_t n = (int64_t)CN_GB_RC * 4 * H;
+    for (int s = 0; s < nseg; ++s) n += (int64_t)T * bwd_part_rows(segs[s].B, bm) * 4 * H;
+    return n;
+}
+
+int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs, float *work)
 {
     if (T <= 0 || H <= 0 || H % GF_BU || nseg < 1 || nseg > 2 || !segs)
         return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: T > 0, H % 32 == 0 and 1 <= nseg <= 2 required");
+    if (!work) return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: null workspace");
     for (int s = 0; s < nseg; ++s) {
         const cn_gru_seq_bwd &q = segs[s];
         if (q.B <= 0) return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: B > 0 required");
-        if (!q.w_hh_t || !q.m || !q.save || !q.hm || !q.acc || !q.g || !q.part)
+        if (!q.w_hh_t || !q.m || !q.save || !q.hm || !q.acc || !q.g || !q.db_ih || !q.db_hh)
             return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: null operand");
         if (!aligned16({q.w_hh_t, q.dout, q.save, q.hm, q.acc, q.g}))
             return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: w_hh_t, dout, save, hm, acc and g must be 16-byte aligned");
     }
     const int ut = H / GF_BU;
-    const int64_t rt0 = cn_gru_seq_tiles(segs[0].B), rt1 = nseg > 1 ? cn_gru_seq_tiles(segs[1].B) : 0;
+    const int64_t bm = row_tile(segs[0].B + (nseg > 1 ? segs[1].B : 0), H);
+    const int64_t rt0 = bwd_part_rows(segs[0].B, bm), rt1 = nseg > 1 ? bwd_part_rows(segs[1].B, bm) : 0;
     const int64_t grid = (rt0 + rt1 + 7) / 8 * 8 * ut;
     if (grid > 0x7fffffff) return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: B too large");
+    float *part[2] = {work, work + (int64_t)T * rt0 * 4 * H};
+    float *red = part[1] + (int64_t)T * rt1 * 4 * H;
     // launch j = 0 .. T: the GEMM of step T - j (none at j = 0) and the gates of step T - 1 - j (none at j = T)
     for (int j = 0; j <= T; ++j) {
         GbArgs P{};
@@ -804,14 +1217,23 @@ int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *s
                     gates ? q.save + tg * 4 * BH : nullptr,
                     gates ? q.hm + tg * BH : nullptr,
                     gates ? q.g + tg * 4 * BH : nullptr,
-                    gates ? q.part + tg * rt * 4 * H : nullptr};
+                    gates ? part[s] + tg * rt * 4 * H : nullptr};
             (s ? P.s1 : P.s0) = g;
         }
         if (nseg == 1) P.s1 = P.s0;
         (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
-        hipLaunchKernelGGL(cn_gru_bwd_fused_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, P);
+        if (bm == SK_BM)
+            hipLaunchKernelGGL(cn_gru_bwd_sk_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, P);
+        else
+            hipLaunchKernelGGL(cn_gru_bwd_fused_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, P);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return cn_set_error(CN_EHIP, hipGetErrorString(e));
+    }
+    // bias gradients: every step's workgroup partials of each GRU, summed in a fixed order
+    for (int s = 0; s < nseg; ++s) {
+        const int rc = cn_gru_bias_reduce(stream, (int64_t)T * (s ? rt1 : rt0), H, part[s], segs[s].db_ih,
+                                          segs[s].db_hh, red);
+        if (rc) return rc;
     }
     return CN_OK;
 }

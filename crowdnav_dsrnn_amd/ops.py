@@ -213,7 +213,7 @@ class _MaskedGRU(torch.autograd.Function):
                                                  out[t].data_ptr(), hn, sv))
         if timing is not None:
             ev1.record()
-            timing.append((B, H, T, ev0, ev1))
+            timing.append((B, H, T, ev0, ev1, 0))
         if need:
             ctx.save_for_backward(x2, m, w_ih, w_hh, hm, save)
         return out, out[-1].clone()
@@ -279,9 +279,9 @@ def _a16(t):
 class _MaskedGRUSeq(torch.autograd.Function):
     """srnn_model.py:52-104 for one or two GRUs of the same T and H (H % 32 == 0) at once: the T-step loops
     run in native code (cn_gru_fwd_seq / cn_gru_bwd_seq, one launch per step for both GRUs: the DSRNN's
-    spatial and temporal edge RNNs share every launch instead of running on two streams). Forward per GRU:
-    gi = x W_ih^T + b_ih as one GEMM over all T*B rows, then the fused recurrent steps (cn_gru_fwd_fused's
-    kernel). Backward: T + 1 launches of the fused recurrent-GEMM + gate-gradient kernel, then the weight /
+    spatial and temporal edge RNNs share every launch instead of running on two streams). Forward: the fused
+    recurrent steps (cn_gru_fwd_fused's kernel), which also project the inputs (x W_ih^T on the MFMA ahead of
+    hm W_hh^T) when F % 32 == 0 (else gi = x W_ih^T + b_ih as one GEMM over all T*B rows first). Backward: T + 1 launches of the fused recurrent-GEMM + gate-gradient kernel, then the weight /
     input gradients as single GEMMs over all T*B rows and the bias partials reduced in a fixed order.
     Inputs: nseg, then per GRU (x, h0, masks, w_ih, w_hh, b_ih, b_hh); outputs per GRU (out, h_T)."""
 
@@ -294,22 +294,30 @@ class _MaskedGRUSeq(torch.autograd.Function):
         dev = segs[0][0].device
         fs = (_lib.GruSeqFwd * nseg)()
         outs, saved, rows = [], [], 0
+        # every input width F % 32 == 0: the step kernel projects x itself (x W_ih^T on the MFMA, gi never
+        # stored); otherwise gi = x W_ih^T + b_ih first (one mode per call)
+        xm = all(sg[0].shape[2] % 32 == 0 for sg in segs)
+        fl = segs[0][0].shape[2] if xm else 0
         for i, (x, h0, masks, w_ih, w_hh, b_ih, b_hh) in enumerate(segs):
             if x.shape[0] != T or w_hh.shape[1] != H:
                 raise ValueError("masked_gru_group: every GRU needs the same T and H")
             B, F = x.shape[1], x.shape[2]
-            x2 = _c(x).reshape(T * B, F)
+            x2 = _a16(x).reshape(T * B, F)
             m = _c(masks).reshape(T, B)
-            gi = torch.addmm(b_ih, x2, w_ih.t())
+            gi = None if xm else torch.addmm(b_ih, x2, w_ih.t())
+            wih, bih = (_a16(w_ih), _a16(b_ih)) if xm else (None, None)
             out = torch.empty((T, B, H), dtype=torch.float32, device=dev)
             nh = T if need else min(T, 2)
             hm = torch.empty((nh, B, H), dtype=torch.float32, device=dev)
             torch.mul(h0, m[0].unsqueeze(-1), out=hm[0])
             save = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev) if need else None
             whh, bhh = _a16(w_hh), _a16(b_hh)
-            fs[i] = _lib.GruSeqFwd(B, gi.data_ptr(), whh.data_ptr(), bhh.data_ptr(), m.data_ptr(), out.data_ptr(),
-                                   hm.data_ptr(), save.data_ptr() if save is not None else None, nh)
-            outs += [out, gi, whh, bhh]
+            fs[i] = _lib.GruSeqFwd(B, gi.data_ptr() if gi is not None else None, whh.data_ptr(), bhh.data_ptr(),
+                                   m.data_ptr(), out.data_ptr(), hm.data_ptr(),
+                                   save.data_ptr() if save is not None else None, nh,
+                                   x2.data_ptr() if xm else None, wih.data_ptr() if xm else None,
+                                   bih.data_ptr() if xm else None, F if xm else 0)
+            outs += [out, gi, whh, bhh, wih, bih]
             saved += [x2, m, w_ih, w_hh, hm, save]
             rows += B
         timing = FUSED_TIMING if (FUSED_TIMING is not None and rows >= FUSED_TIMING_MIN_ROWS) else None
@@ -320,13 +328,13 @@ class _MaskedGRUSeq(torch.autograd.Function):
             _lib.check(L.cn_gru_fwd_seq(_stream(dev), T, H, nseg, fs))
         if timing is not None:
             ev1.record()
-            timing.append((rows, H, T, ev0, ev1))
+            timing.append((rows, H, T, ev0, ev1, fl))
         ctx.nseg = nseg
         if need:
             ctx.save_for_backward(*saved)
         res = []
         for i in range(nseg):
-            out = outs[4 * i]
+            out = outs[6 * i]
             res += [out, out[-1].clone()]
         return tuple(res)
 
@@ -348,25 +356,21 @@ class _MaskedGRUSeq(torch.autograd.Function):
                 torch.zeros((B, H), dtype=torch.float32, device=dev)
             acc = _a16(acc)
             dout = _a16(dout) if dout is not None else None
-            rt = L.cn_gru_seq_tiles(B)
             g = torch.empty((T, B, 4 * H), dtype=torch.float32, device=dev)
-            part = torch.empty((T, rt, 4 * H), dtype=torch.float32, device=dev)
+            db = torch.empty((2, 3 * H), dtype=torch.float32, device=dev)
             wt = w_hh.t().contiguous()
             bs[i] = _lib.GruSeqBwd(B, wt.data_ptr(), m.data_ptr(), dout.data_ptr() if dout is not None else None,
-                                   save.data_ptr(), hm.data_ptr(), acc.data_ptr(), g.data_ptr(), part.data_ptr())
-            keep.append((acc, dout, g, part, wt, rt))
+                                   save.data_ptr(), hm.data_ptr(), acc.data_ptr(), g.data_ptr(), db[0].data_ptr(),
+                                   db[1].data_ptr())
+            keep.append((acc, dout, g, db, wt))
+        work = torch.empty((L.cn_gru_bwd_seq_work_elems(T, H, nseg, bs),), dtype=torch.float32, device=dev)
         with torch.cuda.device(dev):
-            _lib.check(L.cn_gru_bwd_seq(st, T, H, nseg, bs))
+            _lib.check(L.cn_gru_bwd_seq(st, T, H, nseg, bs, work.data_ptr()))
             res = [None]
             for i in range(nseg):
                 x2, m, w_ih, w_hh, hm, save = sv[6 * i:6 * i + 6]
-                acc, _, g, part, _, rt = keep[i]
+                acc, _, g, db, _ = keep[i]
                 B = hm.shape[1]
-                db_ih = torch.empty((3 * H,), dtype=torch.float32, device=dev)
-                db_hh = torch.empty((3 * H,), dtype=torch.float32, device=dev)
-                work = torch.empty((L.cn_gru_bias_work_elems(H),), dtype=torch.float32, device=dev)
-                _lib.check(L.cn_gru_bias_reduce(st, T * rt, H, part.data_ptr(), db_ih.data_ptr(), db_hh.data_ptr(),
-                                                work.data_ptr()))
                 dh0 = acc * m[0].unsqueeze(-1)
                 g2 = g.view(T * B, 4 * H)
                 dgi_nrz, dgh2 = g2[:, :3 * H], g2[:, H:]
@@ -377,7 +381,7 @@ class _MaskedGRUSeq(torch.autograd.Function):
                     dx = (dgi_nrz @ w_ih_nrz).reshape(T, B, -1)
                 dw = wgrad(dgi_nrz, x2)
                 dw_ih = torch.cat((dw[H:], dw[:H]), 0)                       # back to r, z, n
-                res += [dx, dh0, None, dw_ih, wgrad(dgh2, hm.reshape(T * B, H)), db_ih, db_hh]
+                res += [dx, dh0, None, dw_ih, wgrad(dgh2, hm.reshape(T * B, H)), db[0], db[1]]
         return tuple(res)
 
 
@@ -447,6 +451,51 @@ def gru_infer_step(x, h0, m, w_ih, w_hh, b_ih, b_hh, dest):
                                                           hm.data_ptr(), None, out.data_ptr(), None, None, d_ptr, G,
                                                           ld))
     return out
+
+
+def gru_infer_group(*grus):
+    """gru_infer_step for one or two GRUs of the same H (H % 32 == 0) in one launch (cn_gru_fwd_step_group):
+    each argument is (x, h0, m, w_ih, w_hh, b_ih, b_hh, dest) as for gru_infer_step; the input projection runs
+    in the kernel when every x has F % 32 == 0. Returns the new states (R, H) in order."""
+    if not 1 <= len(grus) <= 2:
+        raise ValueError("gru_infer_group: one or two GRUs")
+    x0 = grus[0][0]
+    if not x0.is_cuda:
+        raise EdgeFeaturesUnavailable("gru_infer_group runs only through the HIP step kernels; tensors are on %s"
+                                      % x0.device)
+    H = grus[0][4].shape[1]
+    xm = all(gr[0].shape[-1] % 32 == 0 for gr in grus)
+    segs = (_lib.GruStepSeg * len(grus))()
+    keep, outs = [], []
+    for i, (x, h0, m, w_ih, w_hh, b_ih, b_hh, dest) in enumerate(grus):
+        if w_hh.shape[1] != H or H % 32:
+            raise ValueError("gru_infer_group: every GRU needs the same H, a multiple of 32")
+        h0g = h0 if h0.dim() == 3 else h0.unsqueeze(1)
+        Rg, G = h0g.shape[0], h0g.shape[1]
+        R = Rg * G
+        dev = x.device
+        hm = torch.empty((Rg, G, H), dtype=torch.float32, device=dev)
+        torch.mul(h0g, m.reshape(Rg, 1, 1), out=hm)
+        x2 = _a16(x).reshape(R, -1)
+        F = x2.shape[1]
+        gi = None if xm else torch.addmm(b_ih, x2, w_ih.t())
+        out = torch.empty((R, H), dtype=torch.float32, device=dev)
+        d_ptr, ld = None, 0
+        if dest is not None:
+            dg = dest if dest.dim() == 3 else dest.unsqueeze(1)
+            if tuple(dg.shape) != (Rg, G, H) or dg.stride(2) != 1 or dg.stride(1) != H or dg.dtype != torch.float32:
+                raise ValueError("gru_infer_group: dest must be a float32 (R', G, H) view with rows of H contiguous")
+            d_ptr, ld = dg.data_ptr(), dg.stride(0)
+        wih, bih, whh, bhh = _a16(w_ih), _a16(b_ih), _a16(w_hh), _a16(b_hh)
+        segs[i] = _lib.GruStepSeg(R, gi.data_ptr() if gi is not None else None, x2.data_ptr() if xm else None,
+                                  wih.data_ptr() if xm else None, bih.data_ptr() if xm else None, F if xm else 0,
+                                  hm.data_ptr(), whh.data_ptr(), bhh.data_ptr(), out.data_ptr(), d_ptr, G, ld)
+        keep += [hm, x2, gi, wih, bih, whh, bhh]
+        outs.append(out)
+    dev = x0.device
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().cn_gru_fwd_step_group(_stream(dev), H, len(grus), segs))
+    return outs
 
 
 def gaussian_act(mean, logstd, deterministic=False):

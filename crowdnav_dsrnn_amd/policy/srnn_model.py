@@ -49,6 +49,9 @@ class RNNBase(nn.Module):
         """T = 1 without autograd: ops.gru_infer_step (new state also written into `dest`, which may be a
         slice of the (B, N + 1, H) state tensor and may alias h0)."""
         g = self.gru
+        if x.is_cuda and g.weight_hh_l0.shape[1] % 32 == 0:   # input projection in the step kernel
+            return ops.gru_infer_group((x, h0, m, g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0,
+                                        dest))[0]
         return ops.gru_infer_step(x, h0, m, g.weight_ih_l0, g.weight_hh_l0, g.bias_ih_l0, g.bias_hh_l0, dest)
 
 
@@ -234,8 +237,19 @@ class SRNN(nn.Module):
         else:
             d_edge = out_hxs["human_human_edge_rnn"].view(B, self.num_edges, H)
             d_node = out_hxs["human_node_rnn"].view(B, 1, -1)
-        out_t = self.humanhumanEdgeRNN_temporal.infer_step(te.reshape(B, 64), h_edge[:, 0:1, :], m, d_edge[:, 0:1, :])
-        out_s = self.humanhumanEdgeRNN_spatial.infer_step(se.reshape(B * N, 64), h_edge[:, 1:, :], m, d_edge[:, 1:, :])
+        if te.is_cuda and H % 32 == 0:
+            # both edge RNNs in one launch, the input projections in the kernel (ops.gru_infer_group)
+            gs, gt = self.humanhumanEdgeRNN_spatial.gru, self.humanhumanEdgeRNN_temporal.gru
+            out_s, out_t = ops.gru_infer_group(
+                (se.reshape(B * N, 64), h_edge[:, 1:, :], m, gs.weight_ih_l0, gs.weight_hh_l0, gs.bias_ih_l0,
+                 gs.bias_hh_l0, d_edge[:, 1:, :]),
+                (te.reshape(B, 64), h_edge[:, 0:1, :], m, gt.weight_ih_l0, gt.weight_hh_l0, gt.bias_ih_l0,
+                 gt.bias_hh_l0, d_edge[:, 0:1, :]))
+        else:
+            out_t = self.humanhumanEdgeRNN_temporal.infer_step(te.reshape(B, 64), h_edge[:, 0:1, :], m,
+                                                               d_edge[:, 0:1, :])
+            out_s = self.humanhumanEdgeRNN_spatial.infer_step(se.reshape(B * N, 64), h_edge[:, 1:, :], m,
+                                                              d_edge[:, 1:, :])
         weighted, _ = self.attn(out_t.view(1, B, H), out_s.view(1, B, N, H))
         outputs, _ = self.humanNodeRNN(ne.reshape(1, B, 64), out_t.view(1, B, H), weighted, h_node, m, dest=d_node)
         rnn_hxs["human_node_rnn"] = d_node

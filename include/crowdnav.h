@@ -285,13 +285,34 @@ int cn_gru_bias_reduce(void *stream, int64_t rows, int H, const float *part, flo
 int cn_gaussian_act(void *stream, int64_t E, int A, const float *mean, const float *logstd, const float *eps,
                     float *action, float *logp);
 
+/* One step of up to two GRUs of the same H in one launch (the act() path's temporal and spatial edge RNNs,
+ * srnn_model.py:455-460 at T = 1): cn_gru_fwd_fused per GRU, with the input projection in the kernel when
+ * x is given (gi NULL: x [B][F], w_ih [3H][F], b_ih [3H], F % 32 == 0; every GRU of a call in the same mode)
+ * and the optional grouped copy h_out2 (g2, ld2) of cn_gru_fwd_step_scatter. No mask / save outputs. */
+typedef struct cn_gru_step_seg {
+    int64_t B;
+    const float *gi;
+    const float *x;
+    const float *w_ih;
+    const float *b_ih;
+    int64_t F;
+    const float *hm;     /* [B][H] masked state */
+    const float *w_hh;
+    const float *b_hh;
+    float *h_out;        /* [B][H] */
+    float *h_out2;       /* grouped copy or NULL */
+    int64_t g2;
+    int64_t ld2;
+} cn_gru_step_seg;
+int cn_gru_fwd_step_group(void *stream, int H, int nseg, const cn_gru_step_seg *segs);
+
 /* Whole sequences: the T-step loops of srnn_model.py:52-104's nn.GRU (forward) and of its autograd backward
  * issued from native code, one launch per step for up to two independent GRUs of the same H at once (the
  * DSRNN's spatial and temporal edge RNNs, srnn_model.py:455-460; their rows share each launch). H % 32 == 0;
  * every array 16-byte aligned with rows contiguous; 1 <= nseg <= 2. */
 typedef struct cn_gru_seq_fwd {
     int64_t B;           /* rows */
-    const float *gi;     /* [T][B][3H] = x W_ih^T + b_ih */
+    const float *gi;     /* [T][B][3H] = x W_ih^T + b_ih, or NULL: the kernel projects x itself (below) */
     const float *w_hh;   /* [3H][H] (weight_hh_l0) */
     const float *b_hh;   /* [3H] */
     const float *m;      /* [T][B] masks */
@@ -300,8 +321,13 @@ typedef struct cn_gru_seq_fwd {
                             writes hm[(t + 1) % nh] = h_t * m[t + 1] (nh = T keeps all of them for the backward) */
     float *save;         /* [T][B][4H] r | z | n | gh_n per step for the backward, or NULL */
     int64_t nh;          /* 1 <= nh <= T */
+    const float *x;      /* [T][B][F] GRU inputs when gi is NULL (then gi is never stored: the step kernel runs */
+    const float *w_ih;   /* x W_ih^T on the MFMA ahead of hm W_hh^T); w_ih [3H][F] (weight_ih_l0), b_ih [3H], */
+    const float *b_ih;   /* F % 32 == 0. Every GRU of a call uses the same mode. */
+    int64_t F;
 } cn_gru_seq_fwd;
-/* cn_gru_fwd_fused for t = 0 .. T - 1 (same arithmetic per row and step). */
+/* cn_gru_fwd_fused for t = 0 .. T - 1 (same arithmetic per row and step; like cn_gru_fwd_fused, a launch with
+ * fewer 128-row tiles than CUs splits K over the workgroup's waves on 32-row tiles). */
 int cn_gru_fwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_fwd *segs);
 
 typedef struct cn_gru_seq_bwd {
@@ -315,14 +341,17 @@ typedef struct cn_gru_seq_bwd {
                             out: dL/d hm_0 (the caller multiplies by m[0] for dL/dh0) */
     float *g;            /* [T][B][4H] out: dn | dr | dz | dhn per step (dgh_t = g[t][:, H:4H], dgi_t = g[t][:, 0:3H]
                             in gate order n, r, z) */
-    float *part;         /* [T][cn_gru_seq_tiles(B)][4H] out: bias partials for cn_gru_bias_reduce
-                            (rows = T * cn_gru_seq_tiles(B)) */
+    float *db_ih;        /* [3H] out: the bias gradients (sums over all T * B rows, fixed order) */
+    float *db_hh;        /* [3H] out */
 } cn_gru_seq_bwd;
-int64_t cn_gru_seq_tiles(int64_t B);
+/* floats of workspace cn_gru_bwd_seq needs for these GRUs (reads only the B fields) */
+int64_t cn_gru_bwd_seq_work_elems(int T, int H, int nseg, const cn_gru_seq_bwd *segs);
 /* The backward of cn_gru_fwd_seq: T + 1 launches of one fused kernel, each the recurrent GEMM
  * acc_t = a_t + dgh_t W_hh of one step on the f32 matrix cores with the gate gradients of the step before in
- * its epilogue (cn_gru_bwd_step_gates' arithmetic); replaces the per-step cn_gru_bwd_step_gates + GEMM pair. */
-int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs);
+ * its epilogue (cn_gru_bwd_step_gates' arithmetic; launches with fewer 128-row tiles than CUs split K over
+ * the workgroup's waves on 32-row tiles), then the bias reduction; replaces the per-step
+ * cn_gru_bwd_step_gates + GEMM pair. */
+int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs, float *work);
 
 /* The ConvGRU observation row of every env, obs [E][7 + beams] float32:
  *   [clip(robot (px, py, radius, gx, gy, v_pref, theta) / max_range, 0, 1), scan].

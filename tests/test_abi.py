@@ -34,7 +34,8 @@ def test_library_exports_every_declared_symbol(L):
         assert hasattr(L, sym), sym
 
 
-@pytest.mark.parametrize("cname,py", [("cn_gru_seq_fwd", _lib.GruSeqFwd), ("cn_gru_seq_bwd", _lib.GruSeqBwd)])
+@pytest.mark.parametrize("cname,py", [("cn_gru_seq_fwd", _lib.GruSeqFwd), ("cn_gru_seq_bwd", _lib.GruSeqBwd),
+                                      ("cn_gru_step_seg", _lib.GruStepSeg)])
 def test_gru_seq_structs_match_header(cname, py):
     """The ctypes mirrors of the sequence-GRU argument structs list the header's fields in its order (every
     field 8 bytes: int64_t or a pointer, so the order fixes the layout)."""
@@ -47,14 +48,18 @@ def test_gru_seq_structs_match_header(cname, py):
 
 
 def test_gru_seq_rejects_bad_arguments_without_launching(L):
-    assert L.cn_gru_seq_tiles(1) == 1 and L.cn_gru_seq_tiles(128) == 1 and L.cn_gru_seq_tiles(129) == 2
     segs = (_lib.GruSeqFwd * 3)()
     assert L.cn_gru_fwd_seq(None, 4, 256, 3, segs) != 0      # at most two GRUs per call
     assert L.cn_gru_fwd_seq(None, 4, 96 + 4, 1, segs) != 0   # H % 32
     assert L.cn_gru_fwd_seq(None, 4, 256, 1, segs) != 0      # B = 0, null operands
-    bsegs = (_lib.GruSeqBwd * 1)()
-    assert L.cn_gru_bwd_seq(None, 0, 256, 1, bsegs) != 0     # T = 0
-    assert L.cn_gru_bwd_seq(None, 4, 256, 1, bsegs) != 0
+    bsegs = (_lib.GruSeqBwd * 2)()
+    bsegs[0].B, bsegs[1].B = 20480, 2048
+    # workspace: bias partials of 128-row tiles ((160 + 16) x 4H per step) + the reduction's 64 x 4H
+    assert L.cn_gru_bwd_seq_work_elems(3, 256, 2, bsegs) == (3 * 176 + 64) * 1024
+    bsegs[0].B = 2048   # 16 x 4 tiles of 128 rows < 256 CUs: split-K on 32-row tiles (64 per step)
+    assert L.cn_gru_bwd_seq_work_elems(2, 128, 1, bsegs) == (2 * 64 + 64) * 512
+    assert L.cn_gru_bwd_seq(None, 0, 256, 1, bsegs, None) != 0     # T = 0
+    assert L.cn_gru_bwd_seq(None, 4, 256, 1, bsegs, None) != 0
     assert b"cn_gru_bwd_seq" in L.cn_last_error()
 
 

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from crowdnav_dsrnn_amd import _lib  # noqa: E402
 
 
-def case(name, Bs, H, T=16, reps=3):
+def case(name, Bs, H, T=16, reps=3, F=0):
     L = _lib.lib()
     dev = "cuda:0"
     g = torch.Generator(device=dev)
@@ -22,7 +22,10 @@ def case(name, Bs, H, T=16, reps=3):
     bs = (_lib.GruSeqBwd * len(Bs))()
     keep = []
     for i, B in enumerate(Bs):
-        gi = torch.randn((T, B, 3 * H), generator=g, device=dev)
+        gi = torch.randn((T, B, 3 * H), generator=g, device=dev) if not F else None
+        x = torch.randn((T, B, F), generator=g, device=dev) if F else None
+        wih = torch.randn((3 * H, F), generator=g, device=dev) / max(F, 1) ** 0.5 if F else None
+        bih = torch.randn((3 * H,), generator=g, device=dev) * 0.1 if F else None
         w = torch.randn((3 * H, H), generator=g, device=dev) / H ** 0.5
         b = torch.randn((3 * H,), generator=g, device=dev) * 0.1
         m = (torch.rand((T, B), generator=g, device=dev) > 0.05).float()
@@ -33,12 +36,15 @@ def case(name, Bs, H, T=16, reps=3):
         dout = torch.randn((T, B, H), generator=g, device=dev)
         acc = torch.zeros((B, H), device=dev)
         gg = torch.empty((T, B, 4 * H), device=dev)
-        part = torch.empty((T, L.cn_gru_seq_tiles(B), 4 * H), device=dev)
-        fs[i] = _lib.GruSeqFwd(B, gi.data_ptr(), w.data_ptr(), b.data_ptr(), m.data_ptr(), out.data_ptr(),
-                               hm.data_ptr(), save.data_ptr(), T)
+        db = torch.empty((2, 3 * H), device=dev)
+        fs[i] = _lib.GruSeqFwd(B, gi.data_ptr() if gi is not None else None, w.data_ptr(), b.data_ptr(), m.data_ptr(),
+                               out.data_ptr(), hm.data_ptr(), save.data_ptr(), T,
+                               x.data_ptr() if F else None, wih.data_ptr() if F else None,
+                               bih.data_ptr() if F else None, F)
         bs[i] = _lib.GruSeqBwd(B, wt.data_ptr(), m.data_ptr(), dout.data_ptr(), save.data_ptr(), hm.data_ptr(),
-                               acc.data_ptr(), gg.data_ptr(), part.data_ptr())
-        keep += [gi, w, b, m, out, hm, save, wt, dout, acc, gg, part]
+                               acc.data_ptr(), gg.data_ptr(), db[0].data_ptr(), db[1].data_ptr())
+        keep += [gi, x, wih, bih, w, b, m, out, hm, save, wt, dout, acc, gg, db]
+    work = torch.empty((L.cn_gru_bwd_seq_work_elems(T, H, len(Bs), bs),), device=dev)
 
     def timed(fn, launches):
         fn()
@@ -52,14 +58,17 @@ def case(name, Bs, H, T=16, reps=3):
         return e0.elapsed_time(e1) * 1e3 / reps / launches
 
     tf = timed(lambda: _lib.check(L.cn_gru_fwd_seq(st, T, H, len(Bs), fs)), T)
-    tb = timed(lambda: _lib.check(L.cn_gru_bwd_seq(st, T, H, len(Bs), bs)), T + 1)
+    tb = timed(lambda: _lib.check(L.cn_gru_bwd_seq(st, T, H, len(Bs), bs, work.data_ptr())), T + 1)
     rows = sum(Bs)
     fl = 2.0 * rows * H * 3 * H
+    flf = 2.0 * rows * (H + F) * 3 * H
     print("%-10s rows %6d H %3d: fwd %7.1f us/launch (%.0f TFLOP/s), bwd %7.1f us/launch (%.0f TFLOP/s)"
-          % (name, rows, H, tf, fl / tf / 1e6, tb, fl * T / (T + 1) / tb / 1e6), flush=True)
+          % (name, rows, H, tf, flf / tf / 1e6, tb, fl * T / (T + 1) / tb / 1e6), flush=True)
 
 
 if __name__ == "__main__":
     case("edge pair", (20480, 2048), 256)
+    case("pair, x-mode", (20480, 2048), 256, F=64)
     case("spatial", (20480,), 256)
     case("node", (2048,), 128)
+    case("node x-mode", (2048,), 128, F=128)
