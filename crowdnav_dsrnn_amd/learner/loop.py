@@ -25,7 +25,7 @@ class RolloutTrainer:
         if graphs is None:
             graphs = envs.engine.device.type == "cuda" and os.environ.get("CN_NO_GRAPHS", "") in ("", "0")
         self.graphs = bool(graphs)
-        self._graph, self._warm, self._ep = None, False, None
+        self._graph, self._warm = None, False
         self._ones = self._ep_ret = None
         self.envs = envs
         self.ac = actor_critic
@@ -56,10 +56,10 @@ class RolloutTrainer:
         self.num_updates = max(int(config.training.num_env_steps) // config.ppo.num_steps // nenv, 1)
         self.update_index = 0
 
-    def _rollout(self, ep_sum, ep_cnt):
+    def _rollout(self):
         """num_steps env steps. Per step: act, cn_step, the storage writes (one multi-tensor copy) and one
-        kernel of episode bookkeeping (the returns of the episodes that ended); the episode count and sum
-        are reduced once after the loop (from the stored masks: mask 0 <=> done)."""
+        kernel of episode bookkeeping (the Monitor returns of the episodes that ended, into _ep_ret); collect()
+        reduces the episode count and sum once per rollout, outside any captured graph."""
         r = self.rollouts
         T = r.num_steps
         if self._ones is None or self._ones.shape[0] != self.envs.num_envs:
@@ -75,8 +75,6 @@ class RolloutTrainer:
             masks = torch.rsub(done.unsqueeze(1), 1.0)   # 1 - done as float32 (one kernel)
             r.insert(obs, hxs, action, logp, value, reward.unsqueeze(1), masks, self._ones)
             torch.mul(ep_ret, done, out=self._ep_ret[step])   # Monitor return of the episodes that ended
-        ep_sum += self._ep_ret.sum()
-        ep_cnt += (r.masks[1:] == 0).sum()   # (insert() filled slots 1 .. T of this rollout)
 
     @torch.no_grad()
     def collect(self):
@@ -86,12 +84,6 @@ class RolloutTrainer:
         writes of all steps -- and every rollout from then on is one replay of it: the same kernels on the
         same buffers in the same order, without the ~70 host-side launches per step."""
         r = self.rollouts
-        if self._ep is None:
-            self._ep = (torch.zeros((), dtype=torch.float64, device=self.device),
-                        torch.zeros((), dtype=torch.int64, device=self.device))
-        ep_sum, ep_cnt = self._ep
-        ep_sum.zero_()
-        ep_cnt.zero_()
         if self.graphs and self._warm:
             if self._graph is None:
                 g = torch.cuda.CUDAGraph()
@@ -99,7 +91,7 @@ class RolloutTrainer:
                 try:
                     self.envs.engine.set_graph_mode(True)   # cn_step launches without per-call arguments
                     with torch.cuda.graph(g):   # records only; the replay below runs it
-                        self._rollout(ep_sum, ep_cnt)
+                        self._rollout()
                 except RuntimeError as e:   # a capture-unsafe call on this path: stay eager
                     import warnings
 
@@ -111,10 +103,14 @@ class RolloutTrainer:
         if self.graphs and self._graph is not None:
             self._graph.replay()   # (r.step is back at its start value: num_steps inserts wrap it)
         else:
-            self._rollout(ep_sum, ep_cnt)
+            self._rollout()
             self._warm = True
         self.env_steps += r.num_steps * self.envs.num_envs
-        return ep_sum.clone(), ep_cnt.clone()
+        # episode count and return sum of this rollout, reduced eagerly after it: the mask of slot s + 1 is 0
+        # exactly when env step s ended an episode (insert() filled slots 1 .. T). Kept out of the captured
+        # graph: at C4's shape the captured multi-block reductions of these two sums were seen to return the
+        # other sum's bits on some replays (tools/probe_graph_ep.py)
+        return self._ep_ret.sum(), (r.masks[1:] == 0).sum()
 
     def update(self):
         """One rollout + PPO update. rollout_s / update_s are GPU time between HIP events recorded on the

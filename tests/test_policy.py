@@ -241,6 +241,38 @@ def test_masked_gru_group_vs_fp64(T, Bs, F, H):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("Rg,G,F,H", [(4096, 10, 64, 256), (37, 1, 128, 128), (300, 5, 64, 256), (3, 2, 32, 64)])
+def test_gru_infer_group_vs_infer_step(Rg, G, F, H):
+    """ops.gru_infer_group (one launch for two GRUs, input projection in the kernel; split-K below one
+    workgroup per CU) vs ops.gru_infer_step per GRU (gi GEMM + cn_gru_fwd_fused) on the same operands, the
+    grouped copy into a (R', G + 1, H) state slice included (dest aliasing h0, as in act()). Only the
+    summation order differs: atol 2e-6."""
+    from crowdnav_dsrnn_amd import ops
+
+    dev = "cuda:0"
+    g = torch.Generator(device=dev)
+    g.manual_seed(Rg + G + F + H)
+    state = torch.randn((Rg, G + 1, H), generator=g, device=dev) * 0.5
+    m = (torch.rand((Rg,), generator=g, device=dev) > 0.2).float()
+    xs = [torch.randn((Rg * G, F), generator=g, device=dev), torch.randn((Rg, F), generator=g, device=dev)]
+    ws = [[torch.randn(s, generator=g, device=dev) / s[-1] ** 0.5 for s in ((3 * H, F), (3 * H, H))] +
+          [torch.randn((3 * H,), generator=g, device=dev) * 0.1 for _ in range(2)] for _ in range(2)]
+
+    def args(st, i):
+        sl = st[:, 1:, :] if i == 0 else st[:, 0:1, :]
+        w_ih, w_hh, b_ih, b_hh = ws[i]
+        return (xs[i], sl, m, w_ih, w_hh, b_ih, b_hh, sl)
+
+    st_ref = state.clone()
+    ref = [ops.gru_infer_step(*args(st_ref, i)) for i in range(2)]
+    st_got = state.clone()
+    got = ops.gru_infer_group(args(st_got, 0), args(st_got, 1))
+    torch.cuda.synchronize()
+    for a, b in zip(got + [st_got], ref + [st_ref]):
+        np.testing.assert_allclose(a.cpu().numpy(), b.cpu().numpy(), atol=2e-6, rtol=0)
+
+
+@pytest.mark.gpu
 def test_masked_gru_seq_matches_per_step_path():
     """The native sequence path (cn_gru_fwd_seq / cn_gru_bwd_seq) vs the per-step path it replaced
     (hipBLASLt gi = x W_ih^T + b_ih, then cn_gru_fwd_fused per step; cn_gru_bwd_step_gates + a library GEMM
