@@ -1362,9 +1362,12 @@ __global__ __launch_bounds__(256) void cn_attn_pool_bwd_kernel(int64_t R, int N,
 // row's scores go through LDS (lane 0 of the row writes, the row's lanes read after a barrier).
 // ------------------------------------------------------------------------------------------------
 #define CN_SA_MAXN 64
-#define CN_SA_REG 16
+// NR: a row's first NR edge vectors stay in registers between the two passes (the rest are read again).
+// Instantiated for NR = 10 (N <= 10: C4's rows; backward 79 instead of 103 VGPRs, 6 instead of 4 waves per
+// SIMD: 2.05 -> 1.65 ms at C4's 262,144 x 10 x 256, 3.0 -> 3.75 TB/s; forward 0.90 -> 0.85 ms,
+// tools/probe_attn.py) and NR = 16.
 
-template <int HQ>
+template <int HQ, int NR>
 __global__ __launch_bounds__(256) void cn_spatial_attn_fwd_kernel(int64_t R, int N, float scale,
                                                                   const float *__restrict__ hs,
                                                                   const float *__restrict__ u,
@@ -1381,7 +1384,7 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_fwd_kernel(int64_t R, int
     const float4 uu = ok ? *(const float4 *)(u + r * H + q * 4) : z4;
     const float cr = ok ? c[r] : 0.f;
     const float *hr = hs + (ok ? r : 0) * (int64_t)N * H + q * 4;
-    float4 vc[CN_SA_REG];
+    float4 vc[NR];
     float mx = -INFINITY;
     auto score = [&](int n, const float4 &v) {
         float part = ((uu.x * v.x + uu.y * v.y) + uu.z * v.z) + uu.w * v.w;
@@ -1392,12 +1395,12 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_fwd_kernel(int64_t R, int
         mx = fmaxf(mx, s);
     };
 #pragma unroll
-    for (int n = 0; n < CN_SA_REG; ++n)
+    for (int n = 0; n < NR; ++n)
         if (n < N) {
             vc[n] = ok ? *(const float4 *)(hr + n * H) : z4;
             score(n, vc[n]);
         }
-    for (int n = CN_SA_REG; n < N; ++n) score(n, ok ? *(const float4 *)(hr + n * H) : z4);
+    for (int n = NR; n < N; ++n) score(n, ok ? *(const float4 *)(hr + n * H) : z4);
     __syncthreads();
     float den = 0.f;
     for (int n = 0; n < N; ++n) den += expf(sc[rl][n] - mx);
@@ -1408,9 +1411,9 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_fwd_kernel(int64_t R, int
         if (ok && q == 0) attn[r * N + n] = a;
     };
 #pragma unroll
-    for (int n = 0; n < CN_SA_REG; ++n)
+    for (int n = 0; n < NR; ++n)
         if (n < N) pool(n, vc[n]);
-    for (int n = CN_SA_REG; n < N; ++n) pool(n, ok ? *(const float4 *)(hr + n * H) : z4);
+    for (int n = NR; n < N; ++n) pool(n, ok ? *(const float4 *)(hr + n * H) : z4);
     if (ok) *(float4 *)(out + r * H + q * 4) = acc;
 }
 
@@ -1418,7 +1421,7 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_fwd_kernel(int64_t R, int
 // dscore[n] = scale * attn[n] (p[n] - s) (softmax backward), then
 //   dhs[r][n] = attn[n] dout[r] + dscore[n] u[r],  du[r] = sum_n dscore[n] hs[r][n],  dc[r] = sum_n dscore[n].
 // hs is read once (as forward); dhs written once (it is the spatial GRU output's whole gradient).
-template <int HQ>
+template <int HQ, int NR>
 __global__ __launch_bounds__(256) void cn_spatial_attn_bwd_kernel(int64_t R, int N, float scale,
                                                                   const float *__restrict__ hs,
                                                                   const float *__restrict__ u,
@@ -1439,7 +1442,7 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_bwd_kernel(int64_t R, int
     const float4 g = ok ? *(const float4 *)(dout + r * H + q * 4) : z4;
     const float4 uu = ok ? *(const float4 *)(u + r * H + q * 4) : z4;
     const float *hr = hs + rr * (int64_t)N * H + q * 4;
-    float4 vc[CN_SA_REG];
+    float4 vc[NR];
     float s = 0.f;
     auto grad = [&](int n, const float4 &v) {
         float part = ((g.x * v.x + g.y * v.y) + g.z * v.z) + g.w * v.w;
@@ -1450,12 +1453,12 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_bwd_kernel(int64_t R, int
         s += attn[rr * N + n] * part;
     };
 #pragma unroll
-    for (int n = 0; n < CN_SA_REG; ++n)
+    for (int n = 0; n < NR; ++n)
         if (n < N) {
             vc[n] = ok ? *(const float4 *)(hr + n * H) : z4;
             grad(n, vc[n]);
         }
-    for (int n = CN_SA_REG; n < N; ++n) grad(n, ok ? *(const float4 *)(hr + n * H) : z4);
+    for (int n = NR; n < N; ++n) grad(n, ok ? *(const float4 *)(hr + n * H) : z4);
     __syncthreads();
     float4 acc = z4;
     float dcs = 0.f;
@@ -1470,9 +1473,9 @@ __global__ __launch_bounds__(256) void cn_spatial_attn_bwd_kernel(int64_t R, int
                                                   a * g.w + ds * uu.w);
     };
 #pragma unroll
-    for (int n = 0; n < CN_SA_REG; ++n)
+    for (int n = 0; n < NR; ++n)
         if (n < N) back(n, vc[n]);
-    for (int n = CN_SA_REG; n < N; ++n) back(n, ok ? *(const float4 *)(hr + n * H) : z4);
+    for (int n = NR; n < N; ++n) back(n, ok ? *(const float4 *)(hr + n * H) : z4);
     if (ok) {
         *(float4 *)(du + r * ldu + q * 4) = acc;
         if (q == 0) dc[r * ldc] = dcs;
@@ -1723,15 +1726,19 @@ int cn_spatial_attn_fwd(void *stream, int64_t R, int N, int H, float scale, cons
         return CN_EINVAL;
     const unsigned grid = grid_for(R, H);
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
-    if (H == 256)
-        hipLaunchKernelGGL(cn_spatial_attn_fwd_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, c, out, attn);
-    else if (H == 128)
-        hipLaunchKernelGGL(cn_spatial_attn_fwd_kernel<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, c, out, attn);
-    else
-        hipLaunchKernelGGL(cn_spatial_attn_fwd_kernel<16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, c, out, attn);
+#define CN_SA_FWD(HQ, NR) \
+    hipLaunchKernelGGL((cn_spatial_attn_fwd_kernel<HQ, NR>), dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale, \
+                       hs, u, c, out, attn)
+    if (N <= 10) {
+        if (H == 256) CN_SA_FWD(64, 10);
+        else if (H == 128) CN_SA_FWD(32, 10);
+        else CN_SA_FWD(16, 10);
+    } else {
+        if (H == 256) CN_SA_FWD(64, 16);
+        else if (H == 128) CN_SA_FWD(32, 16);
+        else CN_SA_FWD(16, 16);
+    }
+#undef CN_SA_FWD
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }
@@ -1746,15 +1753,18 @@ int cn_spatial_attn_bwd(void *stream, int64_t R, int N, int H, float scale, cons
         return cn_set_error(CN_EINVAL, "cn_spatial_attn_bwd: bad shape, stride or operand");
     const unsigned grid = grid_for(R, H);
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
-    if (H == 256)
-        hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<64>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, attn, dout, dattn, dhs, du, ldu, dc, ldc);
-    else if (H == 128)
-        hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<32>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, attn, dout, dattn, dhs, du, ldu, dc, ldc);
-    else
-        hipLaunchKernelGGL(cn_spatial_attn_bwd_kernel<16>, dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale,
-                           hs, u, attn, dout, dattn, dhs, du, ldu, dc, ldc);
+#define CN_SA_BWD(HQ, NR) \
+    hipLaunchKernelGGL((cn_spatial_attn_bwd_kernel<HQ, NR>), dim3(grid), dim3(256), 0, (hipStream_t)stream, R, N, scale, hs, u, attn, dout, dattn, dhs, du, ldu, dc, ldc)
+    if (N <= 10) {
+        if (H == 256) CN_SA_BWD(64, 10);
+        else if (H == 128) CN_SA_BWD(32, 10);
+        else CN_SA_BWD(16, 10);
+    } else {
+        if (H == 256) CN_SA_BWD(64, 16);
+        else if (H == 128) CN_SA_BWD(32, 16);
+        else CN_SA_BWD(16, 16);
+    }
+#undef CN_SA_BWD
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? CN_OK : cn_set_error(CN_EHIP, hipGetErrorString(e));
 }
