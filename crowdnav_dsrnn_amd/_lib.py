@@ -125,6 +125,8 @@ def lib():
         L.cn_gru_bwd_step_gates.restype = i32
         L.cn_gru_bias_reduce.argtypes = [vp, i64, ctypes.c_int] + [vp] * 4
         L.cn_gru_bias_reduce.restype = i32
+        L.cn_gae.argtypes = [vp, ctypes.c_int, i64, ctypes.c_float, ctypes.c_float, ctypes.c_int] + [vp] * 5
+        L.cn_gae.restype = i32
         L.cn_gaussian_act.argtypes = [vp, i64, ctypes.c_int] + [vp] * 5
         L.cn_gaussian_act.restype = i32
         L.cn_gru_bwd_seq_work_elems.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqBwd)]
@@ -169,7 +171,7 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_spatial_attn_fwd",
             "cn_spatial_attn_bwd", "cn_wgrad_work_elems", "cn_wgrad",
             "cn_gru_bias_blocks", "cn_gru_bwd_step_bias", "cn_gru_bwd_step_gates", "cn_gru_bias_work_elems", "cn_gru_bias_reduce",
-            "cn_gru_bwd_seq_work_elems", "cn_gru_fwd_step_group", "cn_gru_fwd_seq", "cn_gru_bwd_seq", "cn_gaussian_act",
+            "cn_gru_bwd_seq_work_elems", "cn_gru_fwd_step_group", "cn_gru_fwd_seq", "cn_gru_bwd_seq", "cn_gaussian_act", "cn_gae",
             "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad",
             "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict",
             "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"]

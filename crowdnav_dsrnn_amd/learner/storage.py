@@ -150,7 +150,19 @@ class SRNNRolloutStorage:
         """storage.py:132-177, same operation order (a backward scan over the steps)."""
         T = self.rewards.size(0)
         r, v, m, bm, ret = self.rewards, self.value_preds, self.masks, self.bad_masks, self.returns
-        if use_gae:
+        if use_gae and r.is_cuda and all(t.is_contiguous() and t.dtype == torch.float32 for t in (r, v, m, bm, ret)):
+            # one HIP launch for the whole backward scan (cn_gae), same float32 operation order
+            import ctypes
+
+            from .. import _lib
+
+            v[-1] = next_value
+            E = r[0].numel()
+            with torch.cuda.device(r.device):
+                _lib.check(_lib.lib().cn_gae(ctypes.c_void_p(torch.cuda.current_stream(r.device).cuda_stream), T, E,
+                                             float(gamma), float(gamma * gae_lambda), int(bool(use_proper_time_limits)),
+                                             r.data_ptr(), v.data_ptr(), m.data_ptr(), bm.data_ptr(), ret.data_ptr()))
+        elif use_gae:
             v[-1] = next_value
             gae = torch.zeros_like(next_value)
             for s in reversed(range(T)):

@@ -28,6 +28,7 @@
  *                   library GEMMs
  *   cn_gaussian_act ⟵ the act() tail of DiagGaussian / FixedNormal (distributions.py:36-94): sample or
  *                   mode and the summed log-probability
+ *   cn_gae         ⟵ RolloutStorage.compute_returns with use_gae (storage.py:132-177), one launch per rollout
  *   cn_orca_predict / cn_orca_predict_kd / cn_social_force_predict ⟵ the agent policy plugin
  *                   policy_factory[name](config).predict(JointState) (crowd_nav/policy/policy_factory.py:1-17)
  *   cn_lidar_obs     ⟵ CrowdSimDict.generate_ob's 'convgru' observation (crowd_sim_dict.py:96-101) with
@@ -305,6 +306,13 @@ typedef struct cn_gru_step_seg {
     int64_t ld2;
 } cn_gru_step_seg;
 int cn_gru_fwd_step_group(void *stream, int H, int nseg, const cn_gru_step_seg *segs);
+
+/* Returns by generalized advantage estimation (storage.py:132-177 compute_returns with use_gae), one launch
+ * for the whole rollout: rewards [T][E], values / masks / bad_masks [T + 1][E] (values[T] = next_value),
+ * returns [T + 1][E] (rows 0 .. T-1 written); the reference's float32 operation order per step, with gamma and
+ * gamma_lambda = gamma * gae_lambda as float32 scalars; use_proper_time_limits multiplies by bad_masks. */
+int cn_gae(void *stream, int T, int64_t E, float gamma, float gamma_lambda, int use_proper_time_limits,
+           const float *rewards, const float *values, const float *masks, const float *bad_masks, float *returns);
 
 /* Whole sequences: the T-step loops of srnn_model.py:52-104's nn.GRU (forward) and of its autograd backward
  * issued from native code, one launch per step for up to two independent GRUs of the same H at once (the

@@ -459,3 +459,32 @@ def test_c4_shape_update_properties():
         assert a[3:] == b[3:], u
     for x, y in zip(p_e, p_g):
         np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("E,T,ptl", [(4096, 128, True), (37, 5, False), (1, 1, True)])
+def test_gae_kernel_matches_reference_loop(E, T, ptl):
+    """compute_returns on the GPU (cn_gae, one launch) vs the reference's per-step torch loop
+    (storage.py:132-177) on CPU copies of the same storage: bit-identical returns (same float32 operations in
+    the same order; random episode ends and time-limit masks)."""
+    from crowdnav_dsrnn_amd.learner.storage import SRNNRolloutStorage
+    from tests.helpers import BoxSpace
+
+    g = torch.Generator().manual_seed(E + T)
+    obs_shape = {"robot_node": BoxSpace((1, 7)), "temporal_edges": BoxSpace((1, 2)), "spatial_edges": BoxSpace((3, 2))}
+    st = {}
+    for dev in ("cpu", "cuda:0"):
+        s = SRNNRolloutStorage(T, E, obs_shape, BoxSpace((2,)), 8, 8, device=dev)
+        st[dev] = s
+    r = torch.randn((T, E, 1), generator=g)
+    v = torch.randn((T + 1, E, 1), generator=g)
+    m = (torch.rand((T + 1, E, 1), generator=g) > 0.1).float()
+    bm = (torch.rand((T + 1, E, 1), generator=g) > 0.05).float()
+    nv = torch.randn((E, 1), generator=g)
+    for dev, s in st.items():
+        s.rewards.copy_(r)
+        s.value_preds.copy_(v)
+        s.masks.copy_(m)
+        s.bad_masks.copy_(bm)
+        s.compute_returns(nv.to(dev), True, 0.99, 0.95, ptl)
+    assert torch.equal(st["cuda:0"].returns[:-1].cpu(), st["cpu"].returns[:-1])
