@@ -281,8 +281,9 @@ class _MaskedGRUSeq(torch.autograd.Function):
     run in native code (cn_gru_fwd_seq / cn_gru_bwd_seq, one launch per step for both GRUs: the DSRNN's
     spatial and temporal edge RNNs share every launch instead of running on two streams). Forward: the fused
     recurrent steps (cn_gru_fwd_fused's kernel), which also project the inputs (x W_ih^T on the MFMA ahead of
-    hm W_hh^T) when F % 32 == 0 (else gi = x W_ih^T + b_ih as one GEMM over all T*B rows first). Backward: T + 1 launches of the fused recurrent-GEMM + gate-gradient kernel, then the weight /
-    input gradients as single GEMMs over all T*B rows and the bias partials reduced in a fixed order.
+    hm W_hh^T) when F % 32 == 0 (else gi = x W_ih^T + b_ih as one GEMM over all T*B rows first).
+    Backward: T + 1 launches of the fused recurrent-GEMM + gate-gradient kernel and the bias reduction
+    (cn_gru_bwd_seq), then the weight / input gradients as single GEMMs over all T*B rows.
     Inputs: nseg, then per GRU (x, h0, masks, w_ih, w_hh, b_ih, b_hh); outputs per GRU (out, h_T)."""
 
     @staticmethod
