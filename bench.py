@@ -294,20 +294,19 @@ def dsrnn_flop_per_env_step(N, c):
     return enc + (N + 1) * edge_gru + att + node + heads
 
 
-def run_c4(args, torch, dist, device, rank, world):
+def run_c4(torch, dist, device, rank, world, E, N, K, W):
     """env-steps/s over PPO updates, counted like train.py:342-352 (rollout of num_steps
     steps of every env with DSRNN act() in the loop, then the PPO update, all inside the timed region).
-    A "step" here is one update = 128 x E env steps per GPU. Defaults: 10 timed updates, 2 warmup (eager,
-    then the HIP-graph capture of the rollout)."""
+    A "step" here is one update = 128 x E env steps per GPU; W untimed updates first (the first eager,
+    the second captures the rollout's HIP graph), then K timed ones. Returns the line's dict on rank 0
+    (None elsewhere)."""
+    from crowdnav_dsrnn_amd import ops
     from crowdnav_dsrnn_amd.config import Config, clone_config
     from crowdnav_dsrnn_amd.envs import CrowdNavVecEnv
     from crowdnav_dsrnn_amd.learner import PPO
     from crowdnav_dsrnn_amd.learner.loop import RolloutTrainer
     from crowdnav_dsrnn_amd.policy import Policy
 
-    E, N = args.envs, args.humans
-    K = args.steps if args.steps != 2000 else 10
-    W = args.warmup if args.warmup != 100 else 2   # (the second update captures the rollout graph)
     c = clone_config(Config())
     c.sim.human_num = N
     c.humans.policy = "orca"
@@ -327,34 +326,29 @@ def run_c4(args, torch, dist, device, rank, world):
                 c.ppo.entropy_coef, lr=c.training.lr, eps=c.training.eps, max_grad_norm=c.training.max_grad_norm)
     tr = RolloutTrainer(c, envs, pol, agent)
 
-    def barrier():
-        torch.cuda.synchronize(device)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize(device)
-
-    from crowdnav_dsrnn_amd import ops
-
     for _ in range(W):
         tr.update()
-    barrier()
+    _barrier(torch, dist, device)
     ops.FUSED_TIMING = []   # in-loop HIP events around the spatial-edge GRU's fused steps (its stream)
     t0 = time.perf_counter()
     roll = upd = 0.0
+    episodes = 0
     for _ in range(K):
         st = tr.update()
         roll += st["rollout_s"]
         upd += st["update_s"]
+        episodes += st["episodes"]
         if rank == 0:
             print("c4 update: rollout %.3f s, ppo %.3f s, episodes %d, mean return %.3f, value_loss %.4f"
                   % (st["rollout_s"], st["update_s"], st["episodes"], st["mean_episode_return"],
                      st["value_loss"]), file=sys.stderr, flush=True)
-    barrier()
+    _barrier(torch, dist, device)
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        t = torch.tensor([elapsed, float(episodes)], dtype=torch.float64, device=device)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, episodes = float(t[0].item()), int(t[1].item())
     timing, ops.FUSED_TIMING = ops.FUSED_TIMING, None
     roof = gru_gemm_roofline(torch, device, E // c.ppo.num_mini_batch * N, 256) if rank == 0 else None
     if rank == 0 and timing:
@@ -375,6 +369,7 @@ def run_c4(args, torch, dist, device, rank, world):
                            "the timed updates",
                     isolated_kernel=iso["kernel"], isolated_flop_per_launch=iso["flop_per_launch"],
                     isolated_avg_launch_us=iso["avg_launch_us"])
+    line = None
     if rank == 0:
         steps_per_update = c.ppo.num_steps * E
         fps = dsrnn_flop_per_env_step(N, c)
@@ -396,14 +391,22 @@ def run_c4(args, torch, dist, device, rank, world):
                        "rollout_s_per_update": round(roll / K, 4), "ppo_s_per_update": round(upd / K, 4),
                        "rollout_timing": "HIP events on the update's stream (rollout = act + cn_step + storage, "
                                          "incl. get_value / compute_returns; ppo = PPO.update)",
+                       "resets": episodes,
                        "parallelism": "dp%d (env-sharded%s)" % (world, ", PPO grads all-reduced" if world > 1 else "")},
             "roofline": roof,
             "whole_update_roofline": whole,
         }
-        print(json.dumps(line), flush=True)
     envs.close()
+    del tr, agent, pol, envs
+    torch.cuda.empty_cache()
+    return line
+
+
+def _barrier(torch, dist, device):
+    torch.cuda.synchronize(device)
     if dist is not None:
-        dist.destroy_process_group()
+        dist.barrier()
+    torch.cuda.synchronize(device)
 
 
 def reset_total(eng):
@@ -415,31 +418,25 @@ def reset_total(eng):
     return int(sum(int(v.reset_count.astype(np.int64).sum()) for v in views))
 
 
-_HIP = None
-
-
 def reset_total_dev(eng):
-    """reset_total of a plain engine from its reset_count field alone (E x 4 bytes read straight from the
-    device blob with a synchronous hipMemcpy), so the window that follows does not start behind a 15 MB
-    pageable state copy; mixed engines fall back to reset_total."""
-    global _HIP
+    """reset_total of a plain engine from its reset_count field alone: the E x 4 bytes of that field are
+    copied on the device by the engine library itself (cn_debug_copy64, stream-ordered after the steps) into
+    a torch tensor and summed there, so the window that follows does not start behind a 15 MB pageable
+    state copy and no second handle on the HIP runtime is needed; mixed engines fall back to reset_total."""
+    import torch
+
     from crowdnav_dsrnn_amd import _lib, abi
 
     if eng.groups is not None:
         return reset_total(eng)
-    if _HIP is None:
-        _HIP = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch already loaded (soname match)
-        _HIP.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     off = abi.state_layout(eng.E, eng.N, eng.cfg.robot_visible)[0]["reset_count"][0]
     base = _lib.lib().cn_state_device_ptr(eng._h)
-    out = np.zeros(eng.E, np.int32)
-    import torch
-
-    torch.cuda.synchronize(eng.device)
-    rc = _HIP.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(base + off), out.nbytes, 2)
-    if rc != 0:
-        raise RuntimeError("hipMemcpy of reset_count failed (%d)" % rc)
-    return int(out.astype(np.int64).sum())
+    n64 = (eng.E + 1) // 2   # the field is padded to 256 B: the odd-E tail word stays inside it
+    buf = torch.empty((2 * n64,), dtype=torch.int32, device=eng.device)
+    with torch.cuda.device(eng.device):
+        st = ctypes.c_void_p(torch.cuda.current_stream(eng.device).cuda_stream)
+        _lib.check(_lib.lib().cn_debug_copy64(st, n64, 64, ctypes.c_void_p(base + off), ctypes.c_void_p(buf.data_ptr())))
+    return int(buf[:eng.E].to(torch.int64).sum().item())
 
 
 def launch_plan(gpus, environ):
@@ -490,6 +487,104 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng="mt19937"):
+    """The env hot path alone (c2 / c3 / c5): W untimed launches after cn_reset, then K timed ones
+    (barrier + synchronize on both sides, max over ranks); with `steady` also SURVEY §8d's window on the
+    same engine (100 more warm-up launches, then 2,000 timed ones). Returns the measurements on every rank."""
+    from crowdnav_dsrnn_amd import _lib
+    from crowdnav_dsrnn_amd.engine import CrowdNavEngine
+
+    if workload == "c5":
+        cfgs, env_group = c5_mixed(E, rank * E, E * world, rng)
+        engs = [CrowdNavEngine.mixed(cfgs, env_group, device)]
+    else:
+        engs = [CrowdNavEngine(make_config(E, N, rank * E, E * world, workload, rng), device)]
+    eng = engs[0]
+    SW, SK = 100, 2000   # SURVEY §8d: 100 warm-up steps, then >= 2,000 timed steps incl. all auto-resets
+    gen = torch.Generator(device=device)
+    gen.manual_seed(rank)
+
+    def actions(T, e_):
+        if workload == "c2":   # unicycle (dv, dtheta) ~ U[-0.1, 0.1]^2
+            a = torch.rand((T, e_.E, 2), generator=gen, device=device) * 0.2 - 0.1
+        else:                  # holonomic (vx, vy) ~ N(0, 0.5^2), clipped by clip_action in the kernel
+            a = torch.randn((T, e_.E, 2), generator=gen, device=device) * 0.5
+        return a.contiguous()
+
+    acts = [actions(K + W, e_) for e_ in engs]
+    for e_ in engs:
+        e_.reset()
+    for s in range(W):
+        for e_, a in zip(engs, acts):
+            e_.step(a[s])
+    L = _lib.lib()
+
+    def timed_window(acts, first, count):
+        """count launches of every engine, timed between barriers (max over ranks); the step kernel's own
+        time from the two HIP events cn_step records around the window on its stream."""
+        r0 = reset_total_dev(eng)
+        _lib.check(L.cn_profile(eng._h, 1, count))
+        _barrier(torch, dist, device)
+        t0 = time.perf_counter()
+        for s in range(count):
+            for e_, a in zip(engs, acts):
+                e_.step(a[first + s])
+        _barrier(torch, dist, device)
+        elapsed = time.perf_counter() - t0
+        a_ms, b_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        _lib.check(L.cn_profile_read(eng._h, ctypes.byref(a_ms), ctypes.byref(b_ms), ctypes.byref(n)))
+        _lib.check(L.cn_profile(eng._h, 0, 0))
+        resets = reset_total_dev(eng) - r0
+        if dist is not None:
+            t = torch.tensor([elapsed, float(resets)], dtype=torch.float64, device=device)
+            dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+            elapsed, resets = float(t[0].item()), int(t[1].item())
+        return elapsed, a_ms.value / 1e3 / max(n.value, 1), resets
+
+    out = {"workload": workload, "W": W, "K": K}
+    out["main"] = timed_window(acts, W, K)
+    out["done_frac"] = float(eng.done.float().mean().item())   # envs that ended an episode at the last step
+    out["steady"] = None
+    if steady:
+        del acts
+        sacts = [actions(SW + SK, e_) for e_ in engs]
+        for s in range(SW):
+            for e_, a in zip(engs, sacts):
+                e_.step(a[s])
+        out["steady"] = timed_window(sacts, SW, SK)
+        out["SW"], out["SK"] = SW, SK
+        del sacts
+    out["E_total"] = sum(e_.E for e_ in engs)
+    out["N"] = N
+    if workload == "c5":   # per group: its envs x B_step(its own N) (padding rows not counted)
+        hum = eng.env_humans.cpu().numpy()
+        out["bpl"] = int(sum(algorithmic_bytes_per_env_step(int(n)) for n in hum))
+    else:
+        out["bpl"] = algorithmic_bytes_per_env_step(eng.N) * eng.E
+    for e_ in engs:
+        e_.close()
+    return out
+
+
+def env_window_obj(m, world, which="main"):
+    """The line's object for one window of run_env (value, timing, resets, roofline)."""
+    el, ks, resets = m[which]
+    W, K = (m["W"], m["K"]) if which == "main" else (m["W"] + m["K"] + m["SW"], m["SK"])
+    pmc = load_pmc("cn_step_kernel", m["workload"], window=(W, K))
+    return {"value": round(world * m["E_total"] * K / el, 1), "unit": "env-steps/s", "warmup": W, "steps": K,
+            "ms_per_step": round(el / K * 1e3, 6), "step_kernel_ms": round(ks * 1e3, 5),
+            "window": "launches %d..%d after cn_reset" % (W + 1, W + K), "launches": [W, K], "resets": resets,
+            "roofline": roofline_obj(m["bpl"] / ks / 1e9, m["bpl"], pmc)}
+
+
+# SURVEY §8d side measurements carried by the default line (VERDICT r04: driver-observed C3 / C4 / C5):
+# (workload, warm-up, timed steps); C4 counts PPO updates (the first warm-up update runs eagerly, the second
+# captures the rollout's HIP graph)
+SIDE_WINDOWS = (("c3", 100, 200), ("c5", 100, 200), ("c4", 2, 2))
+SIDE_DEADLINE_S = 300.0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -499,6 +594,7 @@ def main():
     ap.add_argument("--humans", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-steady", action="store_true", help="skip the steady_state window (100 + 2000 launches)")
+    ap.add_argument("--no-side", action="store_true", help="skip the C3 / C4 / C5 side windows of the c2 line")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--rng", choices=["mt19937", "philox"], default="mt19937",
                     help="reset / goal-change stream: mt19937 = the reference's numpy draws (default, the "
@@ -532,141 +628,114 @@ def main():
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
 
-    from crowdnav_dsrnn_amd import _lib
-    from crowdnav_dsrnn_amd.engine import CrowdNavEngine
-
     E, N, K, W = args.envs, args.humans, args.steps, args.warmup
     if args.workload == "c4":
-        return run_c4(args, torch, dist, device, rank, world)
+        line = run_c4(torch, dist, device, rank, world, E, N, K if K != 2000 else 10, W if W != 100 else 2)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     if args.workload == "c3" and N == 10:
         N = 25
     if args.workload == "c5" and E == 4096:
         E = 8192
     if args.workload == "c5":
         N = 5
-        cfgs, env_group = c5_mixed(E, rank * E, E * world, args.rng)
-        engs = [CrowdNavEngine.mixed(cfgs, env_group, device)]
-    else:
-        engs = [CrowdNavEngine(make_config(E, N, rank * E, E * world, args.workload, args.rng), device)]
-    eng = engs[0]
-    SW, SK = 100, 2000   # 100 warm-up steps, then >= 2,000 timed steps incl. all auto-resets
-    steady = not args.no_steady and (K < SK or W < SW)
-    gen = torch.Generator(device=device)
-    gen.manual_seed(rank)
-
-    def actions(T, e_):
-        if args.workload == "c2":   # unicycle (dv, dtheta) ~ U[-0.1, 0.1]^2
-            a = torch.rand((T, e_.E, 2), generator=gen, device=device) * 0.2 - 0.1
-        else:                       # holonomic (vx, vy) ~ N(0, 0.5^2), clipped by clip_action in the kernel
-            a = torch.randn((T, e_.E, 2), generator=gen, device=device) * 0.5
-        return a.contiguous()
-
-    acts = [actions(K + W, e_) for e_ in engs]
-    for e_ in engs:
-        e_.reset()
-    for s in range(W):
-        for e_, a in zip(engs, acts):
-            e_.step(a[s])
-    L = _lib.lib()
-
-    def barrier():
-        torch.cuda.synchronize(device)
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize(device)
-
-    def timed_window(acts, first, count):
-        """count launches of every engine, timed between barriers (max over ranks); the step kernel's own
-        time from the two HIP events cn_step records around the window on its stream."""
-        r0 = reset_total_dev(eng)
-        _lib.check(L.cn_profile(eng._h, 1, count))
-        barrier()
-        t0 = time.perf_counter()
-        for s in range(count):
-            for e_, a in zip(engs, acts):
-                e_.step(a[first + s])
-        barrier()
-        elapsed = time.perf_counter() - t0
-        a_ms, b_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
-        _lib.check(L.cn_profile_read(eng._h, ctypes.byref(a_ms), ctypes.byref(b_ms), ctypes.byref(n)))
-        _lib.check(L.cn_profile(eng._h, 0, 0))
-        resets = reset_total_dev(eng) - r0
-        if dist is not None:
-            t = torch.tensor([elapsed, float(resets)], dtype=torch.float64, device=device)
-            dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
-            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-            elapsed, resets = float(t[0].item()), int(t[1].item())
-        return elapsed, a_ms.value / 1e3 / max(n.value, 1), resets
-
-    elapsed, kernel_s, resets = timed_window(acts, W, K)
-    done_frac = float(eng.done.float().mean().item())   # envs that ended an episode at the window's last step
-    st_win = None
-    if steady:
-        del acts
-        sacts = [actions(SW + SK, e_) for e_ in engs]
-        for s in range(SW):
-            for e_, a in zip(engs, sacts):
-                e_.step(a[s])
-        st_win = timed_window(sacts, SW, SK)
-        del sacts
-
-    E_total = sum(e_.E for e_ in engs)
-    if args.workload == "c5":   # per group: its envs x B_step(its own N) (padding rows not counted)
-        hum = eng.env_humans.cpu().numpy()
-        bpl = int(sum(algorithmic_bytes_per_env_step(int(n)) for n in hum))
-    else:
-        bpl = algorithmic_bytes_per_env_step(eng.N) * eng.E
+    steady = not args.no_steady and (K < 2000 or W < 100)
+    m = run_env(torch, dist, device, rank, world, args.workload, E, N, K, W, steady, args.rng)
+    line = None
     if rank == 0:
-        value = world * E_total * K / elapsed
-        achieved = bpl / kernel_s / 1e9   # c5: kernel_s = both group launches of a step
-        pmc = load_pmc("cn_step_kernel", args.workload, window=(W, K))
+        main_w = env_window_obj(m, world)
         line = {
             "metric": METRIC,
-            "value": round(value, 1),
+            "value": main_w["value"],
             "unit": "env-steps/s",
             "n_gpus": world,
             "steps": K,
             "warmup": W,
-            "ms_per_step": round(elapsed / K * 1e3, 6),
+            "ms_per_step": main_w["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": WORKLOAD_DESC[args.workload] % (E_total, N),
-                "envs_per_gpu": E_total, "humans": N if args.workload != "c5" else "5 (traffic) / 1 (side_pref)",
-                "global_envs": E_total * world,
+                "workload": WORKLOAD_DESC[args.workload] % (m["E_total"], N),
+                "envs_per_gpu": m["E_total"], "humans": N if args.workload != "c5" else "5 (traffic) / 1 (side_pref)",
+                "global_envs": m["E_total"] * world,
                 "parallelism": "env-sharded x%d (no collective)" % world,
                 "rng": args.rng,
-                "step_kernel_ms": round(kernel_s * 1e3, 5),
-                "window": "launches %d..%d after cn_reset" % (W + 1, W + K),
-                "launches": [W, K],
-                "resets": resets,
-                "done_frac_last_step": round(done_frac, 5),
+                "step_kernel_ms": main_w["step_kernel_ms"],
+                "window": main_w["window"],
+                "launches": main_w["launches"],
+                "resets": main_w["resets"],
+                "done_frac_last_step": round(m["done_frac"], 5),
             },
-            "roofline": roofline_obj(achieved, bpl, pmc),
+            "roofline": main_w["roofline"],
         }
-        if st_win is not None:
-            s_el, s_ks, s_resets = st_win
-            s_pmc = load_pmc("cn_step_kernel", args.workload, window=(W + K + SW, SK))
-            line["steady_state"] = {
-                "value": round(world * E_total * SK / s_el, 1), "unit": "env-steps/s",
-                "warmup": SW, "steps": SK, "ms_per_step": round(s_el / SK * 1e3, 6),
-                "step_kernel_ms": round(s_ks * 1e3, 5),
-                "window": "launches %d..%d after cn_reset (SURVEY 8d: 100 warm-up + 2000 timed, incl. auto-resets)"
-                          % (W + K + SW + 1, W + K + SW + SK),
-                "launches": [W + K + SW, SK],
-                "resets": s_resets,
-                "roofline": roofline_obj(bpl / s_ks / 1e9, bpl, s_pmc),
-            }
+        if m["steady"] is not None:
+            st = env_window_obj(m, world, "steady")
+            st["window"] += " (SURVEY 8d: 100 warm-up + 2000 timed, incl. auto-resets)"
+            line["steady_state"] = st
+    if args.workload == "c2" and not args.no_side:
+        run_side_windows(torch, dist, device, rank, world, args.rng, line)
+    if rank == 0:
         if not args.no_cpu_baseline and world == 1 and args.workload == "c2":
             line["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
         print(json.dumps(line), flush=True)
-    for e_ in engs:
-        e_.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_side_windows(torch, dist, device, rank, world, rng, line):
+    """SIDE_WINDOWS into line["side_c3"], ["side_c4"], ["side_c5"] (rank 0), each workload at its SURVEY §8d
+    per-GPU shape on the same ranks. A watchdog bounds them: past SIDE_DEADLINE_S every rank stops, rank 0
+    prints the line with what it has (the side windows never cost the main line)."""
+    import threading
+
+    t_start = time.perf_counter()
+
+    def bail():
+        if rank == 0 and line is not None:
+            line["side_timeout_s"] = SIDE_DEADLINE_S
+            print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
+
+    timer = threading.Timer(SIDE_DEADLINE_S, bail)
+    timer.daemon = True
+    timer.start()
+    try:
+        for wl, w, k in SIDE_WINDOWS:
+            t0 = time.perf_counter()
+            try:
+                if wl == "c4":
+                    obj = run_c4(torch, dist, device, rank, world, 4096, 10, k, w)
+                    if obj is not None:
+                        obj = {"workload": obj["config"]["workload"], "value": obj["value"], "unit": obj["unit"],
+                               "warmup": w, "steps": k, "step": "one rollout of 128 steps of every env + one PPO update",
+                               "ms_per_step": obj["ms_per_step"], "resets": obj["config"]["resets"],
+                               "rollout_s_per_update": obj["config"]["rollout_s_per_update"],
+                               "ppo_s_per_update": obj["config"]["ppo_s_per_update"],
+                               "roofline": obj["roofline"], "whole_update_roofline": obj["whole_update_roofline"]}
+                else:
+                    E, N = (4096, 25) if wl == "c3" else (8192, 5)
+                    m = run_env(torch, dist, device, rank, world, wl, E, N, k, w, False, rng)
+                    obj = None
+                    if rank == 0:
+                        obj = dict(env_window_obj(m, world), workload=WORKLOAD_DESC[wl] % (m["E_total"], N))
+            except Exception as e:   # reported in the line; the main measurement stands
+                obj = {"error": "%s: %s" % (type(e).__name__, e)}
+            torch.cuda.empty_cache()
+            if rank == 0:
+                obj["wall_s"] = round(time.perf_counter() - t0, 2)
+                line["side_" + wl] = obj
+    finally:
+        timer.cancel()
+    if rank == 0:
+        line["side_wall_s"] = round(time.perf_counter() - t_start, 2)
 
 
 def roofline_obj(achieved, bpl, pmc):

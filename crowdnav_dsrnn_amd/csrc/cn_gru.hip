@@ -1002,10 +1002,25 @@ __global__ __launch_bounds__(256) void cn_gru_bwd_sk_kernel(const GbArgs P)
     S.part[(int64_t)rt * 4 * H + q * H + u0 + cu] = s;
 }
 
+// CUs of the current device (256 on the MI355X), read once per device: the split-K choice below, and with
+// it the workspace sizing of cn_gru_bwd_seq_work_elems, follows the part it runs on
+static int device_cus()
+{
+    static int cached[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = n;
+    }
+    return cached[dev];
+}
+
 // 128-row tiles unless that leaves fewer workgroups than CUs (then the split-K kernels, 32-row tiles)
 static inline bool use_split_k(int64_t rows, int H)
 {
-    return (rows + GF_BM - 1) / GF_BM * (H / GF_BU) < 256;
+    return (rows + GF_BM - 1) / GF_BM * (H / GF_BU) < device_cus();
 }
 static inline int64_t row_tile(int64_t rows_total, int H) { return use_split_k(rows_total, H) ? SK_BM : GF_BM; }
 
@@ -1172,6 +1187,10 @@ int cn_gru_fwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_fwd *s
     for (int s = 0; s < nseg; ++s) {
         const cn_gru_seq_fwd &q = segs[s];
         if (q.B <= 0 || q.nh < 1 || q.nh > T) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: B > 0 and 1 <= nh <= T required");
+        // step t reads hm[t % nh] in every workgroup while others write their columns of hm[(t + 1) % nh]: with
+        // nh == 1 and T > 1 those are the same rows (a cross-workgroup race); the backward reads hm of every step
+        if (T > 1 && q.nh < 2) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: nh >= 2 required when T > 1");
+        if (q.save && q.nh != T) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: nh == T required with save");
         if (!q.w_hh || !q.b_hh || !q.m || !q.out || !q.hm) return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: null operand");
         if ((q.x != nullptr) != (segs[0].x != nullptr))
             return cn_set_error(CN_EINVAL, "cn_gru_fwd_seq: every GRU of a call passes gi, or every GRU x / w_ih / b_ih");

@@ -168,7 +168,12 @@ class _MaskedGRU(torch.autograd.Function):
     recurrent GEMM gh = hm W_hh^T + b_hh on the f32 matrix cores with the gates, new state, next masked
     state and the r|z|n|gh_n record for backward in its epilogue; H % 32 != 0: a library GEMM + the
     cn_gru_fwd_step gate kernel). Backward: per step (reversed) one cn_gru_bwd_step and one GEMM acc += dgh W_hh, then the
-    weight / input gradients as single GEMMs over all T*B rows."""
+    weight / input gradients as single GEMMs over all T*B rows.
+
+    masked_gru sends only H % 32 != 0 here (every other H runs _MaskedGRUSeq), so in production this class
+    serves those sizes through its `nblk == 0` branches. The `nblk > 0` branch (cn_gru_bwd_step_gates + a
+    library GEMM per step, H in {64, 128, 256}) is kept as the per-step reference composition the sequence
+    kernels are tested against (tests/test_policy.py::test_masked_gru_seq_matches_per_step_path); nothing else reaches it."""
 
     @staticmethod
     def forward(ctx, x, h0, masks, w_ih, w_hh, b_ih, b_hh):

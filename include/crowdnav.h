@@ -328,7 +328,8 @@ typedef struct cn_gru_seq_fwd {
     float *hm;           /* [nh][B][H] masked states: hm[0] = h0 * m[0] (caller); step t reads hm[t % nh] and
                             writes hm[(t + 1) % nh] = h_t * m[t + 1] (nh = T keeps all of them for the backward) */
     float *save;         /* [T][B][4H] r | z | n | gh_n per step for the backward, or NULL */
-    int64_t nh;          /* 1 <= nh <= T */
+    int64_t nh;          /* 1 <= nh <= T; nh >= 2 when T > 1 (a step's workgroups read hm[t % nh] while others
+                            write hm[(t + 1) % nh]); nh == T when save is not NULL (the backward reads every hm) */
     const float *x;      /* [T][B][F] GRU inputs when gi is NULL (then gi is never stored: the step kernel runs */
     const float *w_ih;   /* x W_ih^T on the MFMA ahead of hm W_hh^T); w_ih [3H][F] (weight_ih_l0), b_ih [3H], */
     const float *b_ih;   /* F % 32 == 0. Every GRU of a call uses the same mode. */
@@ -352,7 +353,8 @@ typedef struct cn_gru_seq_bwd {
     float *db_ih;        /* [3H] out: the bias gradients (sums over all T * B rows, fixed order) */
     float *db_hh;        /* [3H] out */
 } cn_gru_seq_bwd;
-/* floats of workspace cn_gru_bwd_seq needs for these GRUs (reads only the B fields) */
+/* floats of workspace cn_gru_bwd_seq needs for these GRUs (reads only the B fields; the row tiling follows the
+ * current device's CU count, so query on the device the backward runs on) */
 int64_t cn_gru_bwd_seq_work_elems(int T, int H, int nseg, const cn_gru_seq_bwd *segs);
 /* The backward of cn_gru_fwd_seq: T + 1 launches of one fused kernel, each the recurrent GEMM
  * acc_t = a_t + dgh_t W_hh of one step on the f32 matrix cores with the gate gradients of the step before in
