@@ -487,10 +487,13 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
-def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng="mt19937"):
+def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng="mt19937", launch="graph"):
     """The env hot path alone (c2 / c3 / c5): W untimed launches after cn_reset, then K timed ones
     (barrier + synchronize on both sides, max over ranks); with `steady` also SURVEY §8d's window on the
-    same engine (100 more warm-up launches, then 2,000 timed ones). Returns the measurements on every rank."""
+    same engine (100 more warm-up launches, then 2,000 timed ones). launch = "graph" (default): each timed
+    window is one replay of a HIP graph holding its K step launches (cn_set_graph_mode), as RolloutTrainer
+    replays its rollouts, so the window measures the GPU and not the host's Python launch rate; "host":
+    Python issues the K launches inside the timed region. Returns the measurements on every rank."""
     from crowdnav_dsrnn_amd import _lib
     from crowdnav_dsrnn_amd.engine import CrowdNavEngine
 
@@ -519,30 +522,57 @@ def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng=
             e_.step(a[s])
     L = _lib.lib()
 
+    use_graph = launch == "graph" and eng.groups is None   # (mixed engines: host-issued, no graph mode)
+    if use_graph:
+        for e_ in engs:
+            e_.set_graph_mode(True)   # the step sequence on the device: launches capturable (synchronises)
+
     def timed_window(acts, first, count):
-        """count launches of every engine, timed between barriers (max over ranks); the step kernel's own
-        time from the two HIP events cn_step records around the window on its stream."""
+        """count launches of every engine, timed between barriers (max over ranks). launch == "graph": the
+        count launches are captured into one HIP graph first (recorded, not run) and the timed region is its
+        replay; the step kernel's time is the span of two HIP events around the replay on its stream.
+        "host": Python issues every launch inside the timed region; the kernel time from the two HIP events
+        cn_step records around the window on its stream."""
         r0 = reset_total_dev(eng)
-        _lib.check(L.cn_profile(eng._h, 1, count))
+        g = None
+        if use_graph:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for s in range(count):
+                    for e_, a in zip(engs, acts):
+                        e_.step(a[first + s])
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        else:
+            _lib.check(L.cn_profile(eng._h, 1, count))
         _barrier(torch, dist, device)
         t0 = time.perf_counter()
-        for s in range(count):
-            for e_, a in zip(engs, acts):
-                e_.step(a[first + s])
+        if g is not None:
+            ev[0].record()
+            g.replay()
+            ev[1].record()
+        else:
+            for s in range(count):
+                for e_, a in zip(engs, acts):
+                    e_.step(a[first + s])
         _barrier(torch, dist, device)
         elapsed = time.perf_counter() - t0
-        a_ms, b_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
-        _lib.check(L.cn_profile_read(eng._h, ctypes.byref(a_ms), ctypes.byref(b_ms), ctypes.byref(n)))
-        _lib.check(L.cn_profile(eng._h, 0, 0))
+        if g is not None:
+            kernel_s = ev[0].elapsed_time(ev[1]) / 1e3 / count
+            del g
+        else:
+            a_ms, b_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+            _lib.check(L.cn_profile_read(eng._h, ctypes.byref(a_ms), ctypes.byref(b_ms), ctypes.byref(n)))
+            _lib.check(L.cn_profile(eng._h, 0, 0))
+            kernel_s = a_ms.value / 1e3 / max(n.value, 1)
         resets = reset_total_dev(eng) - r0
         if dist is not None:
             t = torch.tensor([elapsed, float(resets)], dtype=torch.float64, device=device)
             dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
             dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
             elapsed, resets = float(t[0].item()), int(t[1].item())
-        return elapsed, a_ms.value / 1e3 / max(n.value, 1), resets
+        return elapsed, kernel_s, resets
 
-    out = {"workload": workload, "W": W, "K": K}
+    out = {"workload": workload, "W": W, "K": K, "launch": "hipGraph replay" if use_graph else "host-issued"}
     out["main"] = timed_window(acts, W, K)
     out["done_frac"] = float(eng.done.float().mean().item())   # envs that ended an episode at the last step
     out["steady"] = None
@@ -575,7 +605,7 @@ def env_window_obj(m, world, which="main"):
     return {"value": round(world * m["E_total"] * K / el, 1), "unit": "env-steps/s", "warmup": W, "steps": K,
             "ms_per_step": round(el / K * 1e3, 6), "step_kernel_ms": round(ks * 1e3, 5),
             "window": "launches %d..%d after cn_reset" % (W + 1, W + K), "launches": [W, K], "resets": resets,
-            "roofline": roofline_obj(m["bpl"] / ks / 1e9, m["bpl"], pmc)}
+            "launch": m["launch"], "roofline": roofline_obj(m["bpl"] / ks / 1e9, m["bpl"], pmc)}
 
 
 # SURVEY §8d side measurements carried by the default line (driver-observed C3 / C4 / C5):
@@ -596,6 +626,9 @@ def main():
     ap.add_argument("--no-steady", action="store_true", help="skip the steady_state window (100 + 2000 launches)")
     ap.add_argument("--no-side", action="store_true", help="skip the C3 / C4 / C5 side windows of the c2 line")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--launch", choices=["graph", "host"], default="graph",
+                    help="timed env windows as one HIP-graph replay of their K step launches (default; the "
+                         "RolloutTrainer path) or as K host-issued launches")
     ap.add_argument("--rng", choices=["mt19937", "philox"], default="mt19937",
                     help="reset / goal-change stream: mt19937 = the reference's numpy draws (default, the "
                          "BASELINE line), philox = fast mode (SURVEY §8f-2)")
@@ -643,7 +676,7 @@ def main():
     if args.workload == "c5":
         N = 5
     steady = not args.no_steady and (K < 2000 or W < 100)
-    m = run_env(torch, dist, device, rank, world, args.workload, E, N, K, W, steady, args.rng)
+    m = run_env(torch, dist, device, rank, world, args.workload, E, N, K, W, steady, args.rng, args.launch)
     line = None
     if rank == 0:
         main_w = env_window_obj(m, world)
@@ -667,6 +700,7 @@ def main():
                 "parallelism": "env-sharded x%d (no collective)" % world,
                 "rng": args.rng,
                 "step_kernel_ms": main_w["step_kernel_ms"],
+                "launch": main_w["launch"],
                 "window": main_w["window"],
                 "launches": main_w["launches"],
                 "resets": main_w["resets"],
@@ -679,7 +713,7 @@ def main():
             st["window"] += " (SURVEY 8d: 100 warm-up + 2000 timed, incl. auto-resets)"
             line["steady_state"] = st
     if args.workload == "c2" and not args.no_side:
-        run_side_windows(torch, dist, device, rank, world, args.rng, line)
+        run_side_windows(torch, dist, device, rank, world, args.rng, line, args.launch)
     if rank == 0:
         if not args.no_cpu_baseline and world == 1 and args.workload == "c2":
             line["cpu_baseline"] = cpu_baseline(N, args.cpu_budget)
@@ -688,7 +722,7 @@ def main():
         dist.destroy_process_group()
 
 
-def run_side_windows(torch, dist, device, rank, world, rng, line):
+def run_side_windows(torch, dist, device, rank, world, rng, line, launch="graph"):
     """SIDE_WINDOWS into line["side_c3"], ["side_c4"], ["side_c5"] (rank 0), each workload at its SURVEY §8d
     per-GPU shape on the same ranks. A watchdog bounds them: past SIDE_DEADLINE_S every rank stops, rank 0
     prints the line with what it has (the side windows never cost the main line)."""
@@ -722,7 +756,7 @@ def run_side_windows(torch, dist, device, rank, world, rng, line):
                                "roofline": obj["roofline"], "whole_update_roofline": obj["whole_update_roofline"]}
                 else:
                     E, N = (4096, 25) if wl == "c3" else (8192, 5)
-                    m = run_env(torch, dist, device, rank, world, wl, E, N, k, w, False, rng)
+                    m = run_env(torch, dist, device, rank, world, wl, E, N, k, w, False, rng, launch)
                     obj = None
                     if rank == 0:
                         obj = dict(env_window_obj(m, world), workload=WORKLOAD_DESC[wl] % (m["E_total"], N))

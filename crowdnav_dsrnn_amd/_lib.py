@@ -138,6 +138,8 @@ def lib():
         L.cn_gru_bwd_seq.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqBwd), vp]
         L.cn_gru_bwd_seq.restype = i32
         L.cn_set_graph_mode.argtypes = [vp, vp, ctypes.c_int]
+        L.cn_graph_node_counts.argtypes = [vp, ctypes.POINTER(i64), ctypes.c_int, ctypes.POINTER(i64)]
+        L.cn_graph_node_counts.restype = i32
         L.cn_wgrad_work_elems.argtypes = [i64, ctypes.c_int, ctypes.c_int]
         L.cn_wgrad_work_elems.restype = i64
         L.cn_wgrad.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int] + [vp] * 6
@@ -158,6 +160,23 @@ def lib():
     return L
 
 
+GRAPH_NODE_TYPES = ("kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event", "event_record",
+                    "ext_sem_signal", "ext_sem_wait", "mem_alloc", "mem_free", "memcpy_from_symbol",
+                    "memcpy_to_symbol")
+
+
+def graph_node_counts(graph):
+    """{node type: count} of a captured hipGraph_t (torch.cuda.CUDAGraph(keep_graph=True).raw_cuda_graph()),
+    through cn_graph_node_counts; types with no node are left out. 'total' = all nodes."""
+    n = len(GRAPH_NODE_TYPES)
+    counts = (ctypes.c_int64 * n)()
+    total = ctypes.c_int64()
+    check(lib().cn_graph_node_counts(ctypes.c_void_p(graph), counts, n, ctypes.byref(total)))
+    out = {GRAPH_NODE_TYPES[k]: int(counts[k]) for k in range(n) if counts[k]}
+    out["total"] = int(total.value)
+    return out
+
+
 def check(rc):
     if rc != 0:
         raise RuntimeError("crowdnav native error %d: %s" % (rc, lib().cn_last_error().decode()))
@@ -172,6 +191,6 @@ EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "c
             "cn_spatial_attn_bwd", "cn_wgrad_work_elems", "cn_wgrad",
             "cn_gru_bias_blocks", "cn_gru_bwd_step_bias", "cn_gru_bwd_step_gates", "cn_gru_bias_work_elems", "cn_gru_bias_reduce",
             "cn_gru_bwd_seq_work_elems", "cn_gru_fwd_step_group", "cn_gru_fwd_seq", "cn_gru_bwd_seq", "cn_gaussian_act", "cn_gae",
-            "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad",
+            "cn_set_graph_mode", "cn_graph_node_counts", "cn_lidar_obs", "cn_debug_disc_quad",
             "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict",
             "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"]

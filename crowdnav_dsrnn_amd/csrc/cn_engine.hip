@@ -3751,7 +3751,40 @@ __global__ void __launch_bounds__(64) cn_sf_predict_kernel(int64_t n, int M, con
     else { out[2 * i] = nx; out[2 * i + 1] = ny; }
 }
 
+// One control word of the engine set from the stream (graph mode's draw-all flag after cn_reset /
+// cn_set_state). A kernel, not hipMemsetAsync: captured into a hipGraph it is a kernel node, and this
+// runtime replays memset nodes with stale bytes (cn_graph_node_counts).
+__global__ void cn_ctl_set_kernel(uint32_t *w, uint32_t v)
+{
+    if (threadIdx.x == 0) *w = v;
+}
+
+static int ctl_set(uint32_t *w, uint32_t v, hipStream_t st)
+{
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(cn_ctl_set_kernel, dim3(1), dim3(64), 0, st, w, v);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : set_err(CN_EHIP, hipGetErrorString(e));
+}
+
 extern "C" {
+
+int cn_graph_node_counts(void *graph, int64_t *counts, int n, int64_t *total)
+{
+    if (!graph || (n > 0 && !counts) || n < 0 || n > 32) return set_err(CN_EINVAL, "cn_graph_node_counts: graph, 0 <= n <= 32");
+    for (int k = 0; k < n; ++k) counts[k] = 0;
+    size_t num = 0;
+    HIPCHK(hipGraphGetNodes((hipGraph_t)graph, nullptr, &num));
+    std::vector<hipGraphNode_t> nodes(num);
+    if (num) HIPCHK(hipGraphGetNodes((hipGraph_t)graph, nodes.data(), &num));
+    for (size_t i = 0; i < num; ++i) {
+        hipGraphNodeType t;
+        HIPCHK(hipGraphNodeGetType(nodes[i], &t));
+        if ((int)t >= 0 && (int)t < n) ++counts[(int)t];
+    }
+    if (total) *total = (int64_t)num;
+    return CN_OK;
+}
 
 const char *cn_last_error(void) { return g_err; }
 #ifndef CN_SRC_HASH
@@ -4095,7 +4128,7 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     // every env starts a new episode: the next step launch draws all next spawns (host flag; graph mode: the
     // device flag, stream-ordered)
     g->pend_all = 1;
-    if (g->devseq) HIPCHK(hipMemsetAsync(g->work_count + CN_CTL_ALL, 1, 4, st));
+    if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, 1u, st);
     return CN_OK;
 }
 
@@ -4244,7 +4277,7 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
     }
     // pending spawns are keyed by (case_counter, reset_count); redraw them for the new state
     g->pend_all = 1;
-    if (g->devseq) HIPCHK(hipMemsetAsync(g->work_count + CN_CTL_ALL, 1, 4, st));
+    if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, 1u, st);
     return CN_OK;
 }
 

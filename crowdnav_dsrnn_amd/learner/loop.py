@@ -26,6 +26,7 @@ class RolloutTrainer:
             graphs = envs.engine.device.type == "cuda" and os.environ.get("CN_NO_GRAPHS", "") in ("", "0")
         self.graphs = bool(graphs)
         self._graph, self._warm = None, False
+        self.graph_audit = None   # node census of the captured rollout graph (collect)
         self._ones = self._ep_ret = None
         self.envs = envs
         self.ac = actor_critic
@@ -86,19 +87,33 @@ class RolloutTrainer:
         r = self.rollouts
         if self.graphs and self._warm:
             if self._graph is None:
-                g = torch.cuda.CUDAGraph()
+                import warnings
+
+                from .. import _lib
+
+                g = torch.cuda.CUDAGraph(keep_graph=True)   # kept until audited, then instantiated
                 step0 = r.step
                 try:
                     self.envs.engine.set_graph_mode(True)   # cn_step launches without per-call arguments
                     with torch.cuda.graph(g):   # records only; the replay below runs it
                         self._rollout()
                 except RuntimeError as e:   # a capture-unsafe call on this path: stay eager
-                    import warnings
-
                     warnings.warn("rollout HIP-graph capture failed (%s); running eagerly" % e)
                     self.graphs = False
                     g = None
                 r.step = step0
+                if g is not None:
+                    # no memset nodes: this ROCm runtime can replay a memset node with stale bytes instead of its
+                    # value (tools/graph_audit.py), e.g. the semaphore of a torch multi-block
+                    # reduction, which then never writes its result
+                    self.graph_audit = _lib.graph_node_counts(g.raw_cuda_graph())
+                    if self.graph_audit.get("memset", 0):
+                        warnings.warn("rollout HIP graph holds %d memset node(s) (%s); running eagerly"
+                                      % (self.graph_audit["memset"], self.graph_audit))
+                        self.graphs = False
+                        g = None
+                    else:
+                        g.instantiate()
                 self._graph = g
         if self.graphs and self._graph is not None:
             self._graph.replay()   # (r.step is back at its start value: num_steps inserts wrap it)
@@ -107,9 +122,10 @@ class RolloutTrainer:
             self._warm = True
         self.env_steps += r.num_steps * self.envs.num_envs
         # episode count and return sum of this rollout, reduced eagerly after it: the mask of slot s + 1 is 0
-        # exactly when env step s ended an episode (insert() filled slots 1 .. T). Kept out of the captured
-        # graph: at C4's shape the captured multi-block reductions of these two sums were seen to return the
-        # other sum's bits on some replays (tools/probe_graph_ep.py)
+        # exactly when env step s ended an episode (insert() filled slots 1 .. T). Not in the captured graph:
+        # torch's multi-block reductions zero their semaphore with hipMemsetAsync, i.e. a memset node, which
+        # this runtime can replay with stale bytes -- round 4 saw the count reduction skip its write and the
+        # count read the sum's bits from the recycled output block (profiles/r05/graph_audit/)
         return self._ep_ret.sum(), (r.masks[1:] == 0).sum()
 
     def update(self):

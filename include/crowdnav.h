@@ -198,8 +198,17 @@ int cn_step(cn_engine *eng, void *stream, const float *actions,
  * per-call arguments and a sequence of cn_step calls (with the caller's other work) can be captured once in
  * a hipGraph and replayed (learner RolloutTrainer). Costs the launch's last workgroup one atomic; off by
  * default (separate kernel variants). Plain engines only (CN_EUNSUPPORTED for cn_create_mixed). Switching
- * synchronises `stream`. No reference equivalent (its env steps are host processes). */
+ * synchronises `stream`. No reference equivalent (its env steps are host processes). The engine issues no
+ * hipMemsetAsync on a stream (graph mode's flag writes are kernels), so a capture never holds a memset node
+ * from it: see cn_graph_node_counts. */
 int cn_set_graph_mode(cn_engine *eng, void *stream, int on);
+
+/* Node census of a captured hipGraph_t (`graph`): counts[k] = nodes of hipGraphNodeType k for k < n (n <= 32;
+ * kernel = 0, memcpy = 1, memset = 2, ...). The rollout trainer refuses to replay a graph that holds memset
+ * nodes: on this ROCm runtime a replayed memset node can write stale bytes instead of its value (DESIGN.md §4,
+ * "HIP-graph memset nodes"), e.g. torch's multi-block reductions then skip writing their result. Returns the
+ * total node count in *total. No reference equivalent. */
+int cn_graph_node_counts(void *graph, int64_t *counts, int n, int64_t *total);
 
 int cn_state_bytes(const cn_engine *eng, int64_t *bytes);
 int cn_state_layout_offsets(const cn_config *cfg, int64_t *offsets, int64_t *total_bytes);

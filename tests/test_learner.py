@@ -369,11 +369,56 @@ def test_rollout_hip_graph_matches_eager():
 
 
 @pytest.mark.gpu
+def test_graph_node_counts_and_memset_free_engine_capture():
+    """cn_graph_node_counts on captured graphs: a torch multi-block reduction (f64 sum of 524,288 values,
+    the round-4 in-graph episode sum) brings memset nodes (its semaphore's hipMemsetAsync) -- the node type
+    this runtime can replay with stale bytes (profiles/r05/graph_audit/memset.log), which RolloutTrainer
+    therefore refuses; the engine's own graph-mode calls (cn_reset, whose draw-all flag is a kernel write,
+    and cn_step) capture as kernel nodes only."""
+    from crowdnav_dsrnn_amd import _lib
+    from crowdnav_dsrnn_amd.engine import CrowdNavEngine
+
+    x = torch.randn((128, 4096), dtype=torch.float64, device="cuda:0")
+    acc = torch.zeros((), dtype=torch.float64, device="cuda:0")
+    acc += x.sum()   # warm-up outside the capture
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g):
+        acc += x.sum()
+    got = _lib.graph_node_counts(g.raw_cuda_graph())
+    assert got.get("memset", 0) >= 1 and got["kernel"] >= 2 and got["total"] == sum(
+        v for k, v in got.items() if k != "total"), got
+    del g
+
+    from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config
+
+    c = clone_config(Config())
+    c.sim.human_num = 5
+    c.humans.policy = "orca"
+    c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+    eng = CrowdNavEngine(make_cn_config(c, num_envs=64, nenv=64, phase="train"), "cuda:0")
+    eng.reset()
+    a = torch.zeros((64, 2), device="cuda:0")
+    eng.step(a)
+    eng.set_graph_mode(True)
+    g2 = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g2):
+        eng.reset()
+        eng.step(a)
+        eng.step(a)
+    got2 = _lib.graph_node_counts(g2.raw_cuda_graph())
+    assert got2 == {"kernel": got2["total"], "total": got2["total"]} and got2["total"] >= 4, got2
+    g2.replay()
+    torch.cuda.synchronize()
+    eng.close()
+
+
+@pytest.mark.gpu
 def test_c4_shape_update_properties():
     """C4's per-GPU shape: 4,096 envs x 10 humans, ORCA, holonomic, 128 steps, 5 epochs,
     2 minibatches, HIP-graph rollouts. Properties at that size (no reference fixture covers it):
-    * graph == eager: three updates from the same start (the graph is captured at the second, replayed at
-      the third) give the same rollouts, losses and parameters bit for bit (deterministic actions);
+    * graph == eager: four updates from the same start (the graph is captured at the second, replayed at
+      the third and fourth) give the same rollouts, losses and parameters bit for bit (deterministic
+      actions), and the captured graph holds no memset node;
     * finite losses and parameters after every update;
     * the Monitor's episode count of each rollout == the number of done flags it stored (masks == 0);
     * the minibatch split of storage.py:228-234: torch.randperm(E) cut into num_mini_batch blocks of
@@ -414,7 +459,7 @@ def test_c4_shape_update_properties():
                     lr=c.training.lr, eps=c.training.eps, max_grad_norm=c.training.max_grad_norm)
         tr = RolloutTrainer(c, envs, pol, agent, deterministic=True, graphs=graphs)
         out = []
-        for u in range(3):
+        for u in range(4):
             st = tr.update()
             r = tr.rollouts
             for k in ("value_loss", "action_loss", "dist_entropy"):
@@ -445,6 +490,8 @@ def test_c4_shape_update_properties():
             allv = torch.cat(seen)
             assert len(seen) == MB and allv.numel() == E4 and torch.equal(torch.sort(allv).values, torch.arange(E4))
         g = tr._graph is not None
+        if graphs:
+            assert tr.graph_audit is not None and not tr.graph_audit.get("memset"), tr.graph_audit
         envs.close()
         del tr, agent, pol, envs
         torch.cuda.empty_cache()

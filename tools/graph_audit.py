@@ -67,6 +67,7 @@ def hip():
         L.hipGraphKernelNodeGetParams.argtypes = [vp, ctypes.POINTER(KernelParams)]
         L.hipGraphDebugDotPrint.argtypes = [vp, ctypes.c_char_p, ctypes.c_uint]
         L.hipMemcpy.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int]
+        L.hipMemsetAsync.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, vp]
         _HIP = L
     return _HIP
 
@@ -150,30 +151,121 @@ def read_words(addr, n=1):
     return list(buf)
 
 
+def dot_names(txt):
+    """{node index: label} of a hipGraphDebugDotPrint dump (kernel nodes: the mangled kernel name)."""
+    out = {}
+    for i, lab in re.findall(r'"graph_0_node_(\d+)"\[[^\]]*?label="\d+\n(.*?)"\];', txt, re.S):
+        out[int(i)] = lab.strip().split("\n")[0]
+    return out
+
+
 def report(tag, graph):
     os.makedirs(OUT, exist_ok=True)
     nodes = walk(graph)
     s = summarize(nodes)
     dpath = os.path.join(OUT, "%s.dot" % tag)
+    names = {}
     try:
         _, txt = dot(graph, dpath)
         s["dot"] = os.path.relpath(dpath, REPO)
-        s["dot_kernel_labels"] = sorted(set(re.findall(r'\\n([A-Za-z_][\w:<>, ]{3,120})\\n', txt)))[:80]
+        names = dot_names(txt)
     except Exception as e:   # the walk above is the evidence; the dump is a convenience
         s["dot_error"] = str(e)
+    for nd in nodes:
+        nd["name"] = names.get(nd["i"], "")
+    kh = {}
+    for nd in nodes:
+        if nd["type"] == "kernel":
+            kh[nd["name"][:110]] = kh.get(nd["name"][:110], 0) + 1
+    s["kernel_histogram"] = dict(sorted(kh.items(), key=lambda kv: -kv[1]))
     json.dump({"summary": s, "nodes": nodes}, open(os.path.join(OUT, "%s.json" % tag), "w"), indent=1, default=str)
-    brief = {k: v for k, v in s.items() if k not in ("memsets", "dot_kernel_labels")}
+    brief = {k: v for k, v in s.items() if k not in ("memsets", "kernel_histogram")}
     print("[%s] %s" % (tag, json.dumps(brief, default=str)), flush=True)
+    for k, v in s["kernel_histogram"].items():
+        print("[%s]   %5d x %s" % (tag, v, k), flush=True)
     for m in s["memsets"]:
-        print("[%s]   memset node %d: dst 0x%x, %d B, value %d, after %s" % (tag, m["i"], m["dst"], m["bytes"],
-                                                                       m["value"], m["prev_type"]), flush=True)
+        i = m["i"]
+        nxt = nodes[i + 1]["name"][:90] if i + 1 < len(nodes) else ""
+        prv = nodes[i - 1]["name"][:90] if i > 0 else ""
+        print("[%s]   memset node %d: dst 0x%x, %d B, value %d, after [%s] before [%s]"
+              % (tag, i, m["dst"], m["bytes"], m["value"], prv, nxt), flush=True)
     return s
 
 
 # ---------------------------------------------------------------------------------------------------------------
+def _alloc_trace():
+    """Allocator events recorded since _record_memory_history was switched on: (action, addr, size)."""
+    snap = torch.cuda.memory._snapshot()
+    out = []
+    for dev_trace in snap.get("device_traces", []):
+        for ev in dev_trace:
+            out.append((ev["action"], ev["addr"], ev["size"]))
+    return out
+
+
 def iso(R=2000):
     """The two round-4 reductions alone: ep_sum += x.sum() (f64, T x E), ep_cnt += (m == 0).sum() (int64),
-    captured once, replayed R times with the accumulators zeroed eagerly before each replay."""
+    captured once and replayed R times. Before each replay the inputs are redrawn in place (so an output a
+    reduction failed to write is stale and shows) and the accumulators zeroed; after it the results are
+    compared with the same reductions run eagerly, and 8 words at each memset destination are read back."""
+    dev = torch.device("cuda:0")
+    T, E = 128, 4096
+    g0 = torch.Generator(device=dev)
+    g0.manual_seed(3)
+    x = torch.randn((T, E), generator=g0, device=dev, dtype=torch.float64)
+    m = (torch.rand((T, E, 1), generator=g0, device=dev) > 0.02).float()
+    ep_s = torch.zeros((), dtype=torch.float64, device=dev)
+    ep_c = torch.zeros((), dtype=torch.int64, device=dev)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):   # warm-up outside capture
+        ep_s += x.sum()
+        ep_c += (m == 0).sum()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    torch.cuda.memory._record_memory_history(max_entries=100000)
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g):
+        ep_s += x.sum()
+        ep_c += (m == 0).sum()
+    trace = _alloc_trace()
+    torch.cuda.memory._record_memory_history(enabled=None)
+    summ = report("iso", g.raw_cuda_graph())
+    for a in trace:
+        print("[iso] allocator during capture: %-14s addr 0x%x size %d" % a, flush=True)
+    sems = [ms["dst"] for ms in summ["memsets"]]
+    bad_s = bad_c = 0
+    hist = {}
+    first = []
+    for r in range(R):
+        x.normal_(generator=g0)
+        m.copy_((torch.rand((T, E, 1), generator=g0, device=dev) > 0.02).float())
+        ep_s.zero_()
+        ep_c.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        words = tuple(tuple(read_words(a, 8)) for a in sems)
+        key = tuple(w[0] for w in words)
+        hist[key] = hist.get(key, 0) + 1
+        want_s, want_c = float(x.sum()), int((m == 0).sum())
+        cs, cc = float(ep_s), int(ep_c)
+        ws, wc = cs != want_s, cc != want_c
+        bad_s += ws
+        bad_c += wc
+        if (ws or wc or r < 3) and len(first) < 12:
+            first.append((r, cs, want_s, cc, want_c, ["%08x" % v for w in words for v in w]))
+    print("[iso] %d replays with fresh inputs: %d wrong sums, %d wrong counts" % (R, bad_s, bad_c), flush=True)
+    print("[iso] first word at each memset destination after the replay: %s" % {str(k): v for k, v in hist.items()},
+          flush=True)
+    for f in first:
+        print("[iso]   replay %d: sum %r (eager %r) count %d (eager %d); words at memset dsts %s" % f, flush=True)
+
+
+def iso_const(R=2000, sentinel=False):
+    """The round-4 reductions with CONSTANT inputs and only the accumulators' zero fills between replays (the
+    first probe's condition, under which the second memset's destination read 0x01010141 after every replay
+    but the first). sentinel=True: the two sums go to preallocated outputs that are filled with a sentinel
+    (NaN / -7) before each replay, so a reduction that does not write its output shows."""
     dev = torch.device("cuda:0")
     T, E = 128, 4096
     g0 = torch.Generator(device=dev)
@@ -183,35 +275,103 @@ def iso(R=2000):
     want_s, want_c = float(x.sum()), int((m == 0).sum())
     ep_s = torch.zeros((), dtype=torch.float64, device=dev)
     ep_c = torch.zeros((), dtype=torch.int64, device=dev)
+    s_out = torch.zeros((), dtype=torch.float64, device=dev)
+    c_out = torch.zeros((), dtype=torch.int64, device=dev)
+
+    def body():
+        if sentinel:
+            torch.sum(x, dim=(0, 1), out=s_out)
+            torch.sum(m == 0, dim=(0, 1, 2), out=c_out)
+            ep_s.add_(s_out)
+            ep_c.add_(c_out)
+        else:
+            ep_s.add_(x.sum())
+            ep_c.add_((m == 0).sum())
+
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):   # warm-up outside capture
-        ep_s += x.sum()
-        ep_c += (m == 0).sum()
+    with torch.cuda.stream(s):
+        body()
     torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g):
-        ep_s += x.sum()
-        ep_c += (m == 0).sum()
-    summ = report("iso", g.raw_cuda_graph())
+        body()
+    tag = "iso_sentinel" if sentinel else "iso_const"
+    summ = report(tag, g.raw_cuda_graph())
     sems = [ms["dst"] for ms in summ["memsets"]]
-    bad = []
-    hist = {}
+    hist, bad, unwritten, first = {}, 0, [0, 0], []
     for r in range(R):
         ep_s.zero_()
         ep_c.zero_()
+        if sentinel:
+            s_out.fill_(float("nan"))
+            c_out.fill_(-7)
         g.replay()
         torch.cuda.synchronize()
-        words = tuple(read_words(a)[0] for a in sems)
-        hist[words] = hist.get(words, 0) + 1
+        words = tuple(tuple(read_words(a, 4)) for a in sems)
+        key = tuple(w[0] for w in words)
+        hist[key] = hist.get(key, 0) + 1
         cs, cc = float(ep_s), int(ep_c)
-        if cs != want_s or cc != want_c:
-            bad.append((r, cs, cc, words))
-    print("[iso] %d replays, %d wrong; semaphore words after replay: %s" % (R, len(bad), {str(k): v for k, v in hist.items()}),
-          flush=True)
-    for b in bad[:10]:
-        print("[iso]   replay %d: sum %r count %d (want %r, %d); words %s" % (b[0], b[1], b[2], want_s, want_c, b[3]),
+        wrong = cs != want_s or cc != want_c
+        bad += wrong
+        if sentinel:
+            unwritten[0] += s_out.isnan().item()
+            unwritten[1] += int(c_out.item()) == -7
+        if (wrong or r < 3 or (r > 0 and key != first[-1][-1] if first else False)) and len(first) < 12:
+            first.append((r, cs, cc, key))
+    print("[%s] %d replays (constant inputs, want sum %r count %d): %d wrong; outputs left unwritten: %s"
+          % (tag, R, want_s, want_c, bad, unwritten if sentinel else "n/a"), flush=True)
+    print("[%s] first word at each memset destination after the replay: %s"
+          % (tag, {"(" + ", ".join("0x%08x" % v for v in k) + ")": n for k, n in hist.items()}), flush=True)
+    for f in first:
+        print("[%s]   replay %d: sum %r count %d; memset words %s" % ((tag,) + f[:3] + (["0x%08x" % v for v in f[3]],)),
               flush=True)
+
+
+def memset_probe(R=2000):
+    """Memset nodes alone: a graph of hipMemsetAsync(value 0) nodes (4 and 16 bytes) around one small
+    kernel, replayed R times; before each replay the destinations are filled with 0x7f7f7f7f eagerly. In the
+    second half an eager hipMemsetAsync(value 1, 4 bytes) to another buffer also precedes each replay (the
+    engine's graph-mode cn_reset / cn_set_state issue exactly that: CN_CTL_ALL = 1). After each replay
+    every destination must read 0."""
+    dev = torch.device("cuda:0")
+    L = hip()
+    A = torch.zeros(4096, dtype=torch.int32, device=dev)
+    Bz = torch.zeros(1024, dtype=torch.int32, device=dev)
+    base = A.data_ptr()
+
+    def ms(off_words, nbytes, value, stream):
+        _ck(L.hipMemsetAsync(ctypes.c_void_p(base + 4 * off_words), value, nbytes,
+                             ctypes.c_void_p(stream.cuda_stream)), "hipMemsetAsync")
+
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g):
+        cs = torch.cuda.current_stream()
+        ms(0, 4, 0, cs)
+        A[512:1024].add_(1)
+        ms(1024, 4, 0, cs)
+        ms(2048, 16, 0, cs)
+    report("memset_probe", g.raw_cuda_graph())
+    bad = [0, 0]
+    seen = {}
+    for r in range(R):
+        A[0:1].fill_(0x7f7f7f7f)
+        A[1024:1025].fill_(0x7f7f7f7f)
+        A[2048:2052].fill_(0x7f7f7f7f)
+        half = r >= R // 2
+        if half:
+            _ck(L.hipMemsetAsync(ctypes.c_void_p(Bz.data_ptr()), 1, 4,
+                                 ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "hipMemsetAsync")
+        g.replay()
+        torch.cuda.synchronize()
+        vals = (int(A[0]), int(A[1024])) + tuple(int(v) for v in A[2048:2052].tolist())
+        if any(vals):
+            bad[half] += 1
+            key = tuple("0x%08x" % (v & 0xffffffff) for v in vals)
+            seen[key] = seen.get(key, 0) + 1
+    print("[memset_probe] %d replays: %d with a nonzero destination without an eager value-1 memset before them, "
+          "%d with one; values seen: %s" % (R, bad[0], bad[1], seen), flush=True)
 
 
 def _trainer(E, old):
@@ -246,6 +406,7 @@ def _trainer(E, old):
                 self._ep[0].add_(self._ep_ret.sum())
                 self._ep[1].add_((self.rollouts.masks[1:] == 0).sum())
 
+        @torch.no_grad()
         def collect(self):
             if old:
                 if getattr(self, "_ep", None) is None:
@@ -300,6 +461,10 @@ if __name__ == "__main__":
     mode = sys.argv[1] if len(sys.argv) > 1 else "iso"
     if mode == "iso":
         iso(int(sys.argv[2]) if len(sys.argv) > 2 else 2000)
+    elif mode == "memset":
+        memset_probe(int(sys.argv[2]) if len(sys.argv) > 2 else 2000)
+    elif mode in ("iso_const", "iso_sentinel"):
+        iso_const(int(sys.argv[2]) if len(sys.argv) > 2 else 2000, sentinel=mode == "iso_sentinel")
     else:
         E = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
         U = int(sys.argv[3]) if len(sys.argv) > 3 else 8
