@@ -487,13 +487,14 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
-def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng="mt19937", launch="graph"):
+def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng="mt19937", launch="seq"):
     """The env hot path alone (c2 / c3 / c5): W untimed launches after cn_reset, then K timed ones
     (barrier + synchronize on both sides, max over ranks); with `steady` also SURVEY §8d's window on the
-    same engine (100 more warm-up launches, then 2,000 timed ones). launch = "graph" (default): each timed
-    window is one replay of a HIP graph holding its K step launches (cn_set_graph_mode), as RolloutTrainer
-    replays its rollouts, so the window measures the GPU and not the host's Python launch rate; "host":
-    Python issues the K launches inside the timed region. Returns the measurements on every rank."""
+    same engine (100 more warm-up launches, then 2,000 timed ones). launch = "seq" (default): each timed
+    window is one cn_step_seq call over its K pre-drawn actions (the K launches go out back to back from
+    native code, so the window measures the GPU and not the host's Python call rate); "host": Python
+    issues the K cn_step calls; "graph": one replay of a HIP graph of the K launches (cn_set_graph_mode).
+    Returns the measurements on every rank."""
     from crowdnav_dsrnn_amd import _lib
     from crowdnav_dsrnn_amd.engine import CrowdNavEngine
 
@@ -527,12 +528,14 @@ def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng=
         for e_ in engs:
             e_.set_graph_mode(True)   # the step sequence on the device: launches capturable (synchronises)
 
+    win_issue = [0.0]
+
     def timed_window(acts, first, count):
-        """count launches of every engine, timed between barriers (max over ranks). launch == "graph": the
-        count launches are captured into one HIP graph first (recorded, not run) and the timed region is its
-        replay; the step kernel's time is the span of two HIP events around the replay on its stream.
-        "host": Python issues every launch inside the timed region; the kernel time from the two HIP events
-        cn_step records around the window on its stream."""
+        """count launches of every engine, timed between barriers (max over ranks). launch == "seq": one
+        cn_step_seq call issues the count launches back to back from native code; "host": Python issues every
+        launch; in both the kernel time comes from the two HIP events cn_step records around the window on its
+        stream. "graph": the count launches are captured into one HIP graph first (recorded, not run) and the
+        timed region is its replay; the kernel time is the span of two HIP events around the replay."""
         r0 = reset_total_dev(eng)
         g = None
         if use_graph:
@@ -550,12 +553,17 @@ def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng=
             ev[0].record()
             g.replay()
             ev[1].record()
+        elif launch == "seq":
+            for e_, a in zip(engs, acts):
+                e_.step_seq(a[first:first + count])
         else:
             for s in range(count):
                 for e_, a in zip(engs, acts):
                     e_.step(a[first + s])
+        t_issued = time.perf_counter()
         _barrier(torch, dist, device)
         elapsed = time.perf_counter() - t0
+        win_issue[0] = t_issued - t0
         if g is not None:
             kernel_s = ev[0].elapsed_time(ev[1]) / 1e3 / count
             del g
@@ -570,9 +578,11 @@ def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng=
             dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
             dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
             elapsed, resets = float(t[0].item()), int(t[1].item())
-        return elapsed, kernel_s, resets
+        return elapsed, kernel_s, resets, win_issue[0]
 
-    out = {"workload": workload, "W": W, "K": K, "launch": "hipGraph replay" if use_graph else "host-issued"}
+    out = {"workload": workload, "W": W, "K": K,
+           "launch": "hipGraph replay" if use_graph else ("cn_step_seq (native loop of cn_step launches)"
+                                                          if launch == "seq" else "host-issued cn_step per step")}
     out["main"] = timed_window(acts, W, K)
     out["done_frac"] = float(eng.done.float().mean().item())   # envs that ended an episode at the last step
     out["steady"] = None
@@ -599,13 +609,18 @@ def run_env(torch, dist, device, rank, world, workload, E, N, K, W, steady, rng=
 
 def env_window_obj(m, world, which="main"):
     """The line's object for one window of run_env (value, timing, resets, roofline)."""
-    el, ks, resets = m[which]
+    el, ks, resets, issue = m[which]
     W, K = (m["W"], m["K"]) if which == "main" else (m["W"] + m["K"] + m["SW"], m["SK"])
     pmc = load_pmc("cn_step_kernel", m["workload"], window=(W, K))
     return {"value": round(world * m["E_total"] * K / el, 1), "unit": "env-steps/s", "warmup": W, "steps": K,
             "ms_per_step": round(el / K * 1e3, 6), "step_kernel_ms": round(ks * 1e3, 5),
             "window": "launches %d..%d after cn_reset" % (W + 1, W + K), "launches": [W, K], "resets": resets,
-            "launch": m["launch"], "roofline": roofline_obj(m["bpl"] / ks / 1e9, m["bpl"], pmc)}
+            "launch": m["launch"],
+            # where the window's wall time goes: the host's time to issue the K launches, the GPU span of the
+            # K step kernels (the two HIP events around them), the rest (first-launch latency + final sync)
+            "window_ms": {"wall": round(el * 1e3, 4), "host_issue": round(issue * 1e3, 4),
+                          "step_kernels": round(ks * K * 1e3, 4), "other": round((el - ks * K) * 1e3, 4)},
+            "roofline": roofline_obj(m["bpl"] / ks / 1e9, m["bpl"], pmc)}
 
 
 # SURVEY §8d side measurements carried by the default line (VERDICT r04: driver-observed C3 / C4 / C5):
@@ -626,9 +641,9 @@ def main():
     ap.add_argument("--no-steady", action="store_true", help="skip the steady_state window (100 + 2000 launches)")
     ap.add_argument("--no-side", action="store_true", help="skip the C3 / C4 / C5 side windows of the c2 line")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
-    ap.add_argument("--launch", choices=["graph", "host"], default="graph",
-                    help="timed env windows as one HIP-graph replay of their K step launches (default; the "
-                         "RolloutTrainer path) or as K host-issued launches")
+    ap.add_argument("--launch", choices=["seq", "host", "graph"], default="seq",
+                    help="timed env windows as one cn_step_seq call (default: K launches back to back from "
+                         "native code), K host-issued cn_step calls, or one HIP-graph replay of the K launches")
     ap.add_argument("--rng", choices=["mt19937", "philox"], default="mt19937",
                     help="reset / goal-change stream: mt19937 = the reference's numpy draws (default, the "
                          "BASELINE line), philox = fast mode (SURVEY §8f-2)")
@@ -722,7 +737,7 @@ def main():
         dist.destroy_process_group()
 
 
-def run_side_windows(torch, dist, device, rank, world, rng, line, launch="graph"):
+def run_side_windows(torch, dist, device, rank, world, rng, line, launch="seq"):
     """SIDE_WINDOWS into line["side_c3"], ["side_c4"], ["side_c5"] (rank 0), each workload at its SURVEY §8d
     per-GPU shape on the same ranks. A watchdog bounds them: past SIDE_DEADLINE_S every rank stops, rank 0
     prints the line with what it has (the side windows never cost the main line)."""

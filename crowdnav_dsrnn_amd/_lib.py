@@ -89,6 +89,7 @@ def lib():
     L.cn_destroy.restype = None
     L.cn_reset.argtypes = [vp, vp, vp, vp, vp]
     L.cn_step.argtypes = [vp, vp, vp] + [vp] * 9
+    L.cn_step_seq.argtypes = [vp, vp, ctypes.c_int, vp, i64] + [vp] * 9
     L.cn_state_bytes.argtypes = [vp, ctypes.POINTER(i64)]
     L.cn_state_layout_offsets.argtypes = [cfgp, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     L.cn_state_field_info.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int),
@@ -151,7 +152,7 @@ def lib():
     L.cn_profile.argtypes = [vp, ctypes.c_int, ctypes.c_int]
     L.cn_profile_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                   ctypes.POINTER(i64)]
-    for f in ("cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans", "cn_reset", "cn_step", "cn_state_bytes", "cn_state_layout_offsets",
+    for f in ("cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans", "cn_reset", "cn_step", "cn_step_seq", "cn_state_bytes", "cn_state_layout_offsets",
               "cn_state_field_info", "cn_get_state", "cn_set_state", "cn_edge_features", "cn_profile",
               "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter", "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_spatial_attn_fwd", "cn_spatial_attn_bwd", "cn_wgrad", "cn_set_graph_mode", "cn_lidar_obs", "cn_debug_disc_quad", "cn_debug_orca", "cn_debug_copy64", "cn_orca_predict", "cn_orca_predict_kd", "cn_social_force_predict", "cn_debug_set_spawn_budget", "cn_debug_spawn_stats"):
         if hasattr(L, f) or not os.environ.get("CN_LIB_PATH"):
@@ -184,7 +185,7 @@ def check(rc):
 
 
 EXPORTED = ["cn_last_error", "cn_version", "cn_config_validate", "cn_create", "cn_create_mixed", "cn_env_humans",
-            "cn_destroy", "cn_reset", "cn_step",
+            "cn_destroy", "cn_reset", "cn_step", "cn_step_seq",
             "cn_state_bytes", "cn_state_layout_offsets", "cn_state_field_info", "cn_get_state", "cn_set_state",
             "cn_state_device_ptr", "cn_edge_features", "cn_profile", "cn_profile_read", "cn_gru_fwd_step", "cn_gru_fwd_step_scatter",
             "cn_gru_fwd_fused", "cn_gru_bwd_step", "cn_attn_pool_fwd", "cn_attn_pool_bwd", "cn_spatial_attn_fwd",

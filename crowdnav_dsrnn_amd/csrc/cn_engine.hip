@@ -4207,6 +4207,21 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     return CN_OK;
 }
 
+int cn_step_seq(cn_engine *g, void *stream, int T, const float *actions, int64_t action_stride, float *robot_node,
+                float *temporal, float *spatial, float *reward, uint8_t *done, int8_t *event, float *info,
+                double *ep_return, int32_t *ep_len)
+{
+    if (!g || !actions) return set_err(CN_EINVAL, "null argument");
+    if (T < 0 || (T > 1 && action_stride < 2 * g->E))
+        return set_err(CN_EINVAL, "cn_step_seq: T >= 0 and action_stride >= 2 * E required");
+    for (int t = 0; t < T; ++t) {
+        const int rc = cn_step(g, stream, actions + (int64_t)t * action_stride, robot_node, temporal, spatial, reward,
+                               done, event, info, ep_return, ep_len);
+        if (rc) return rc;
+    }
+    return CN_OK;
+}
+
 int cn_set_graph_mode(cn_engine *g, void *stream, int on)
 {
     if (!g) return set_err(CN_EINVAL, "null argument");

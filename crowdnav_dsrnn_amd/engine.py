@@ -102,11 +102,7 @@ class CrowdNavEngine:
         # host cost per call matters when a short window starts on an idle GPU: the output pointers and the
         # bound C function are cached, and the device guard is entered only when another device is current
         if self._step_args is None:
-            self._step_fn = _lib.lib().cn_step
-            self._step_args = (self.robot_node.data_ptr(), self.temporal_edges.data_ptr(),
-                               self.spatial_edges.data_ptr(), self.reward.data_ptr(), self.done.data_ptr(),
-                               self.event.data_ptr(), self.info.data_ptr(), self.ep_return.data_ptr(),
-                               self.ep_len.data_ptr())
+            self.step_args()
         if t.cuda.current_device() == self.device.index:
             rc = self._step_fn(self._h, t.cuda.current_stream().cuda_stream, actions.data_ptr(), *self._step_args)
         else:
@@ -114,6 +110,31 @@ class CrowdNavEngine:
                 rc = self._step_fn(self._h, t.cuda.current_stream().cuda_stream, actions.data_ptr(), *self._step_args)
         _lib.check(rc)
         return self.obs(), self.reward, self.done, self.event, self.info, self.ep_return, self.ep_len
+
+    def step_seq(self, actions):
+        """T steps with actions (T, E, 2) f32 (a contiguous device tensor; views along T are fine) issued back to
+        back from native code (cn_step_seq); returns the outputs of the last step, like step()."""
+        t = self.torch
+        if actions.device != self.device or actions.dtype != t.float32 or actions.dim() != 3:
+            raise ValueError("step_seq: actions must be a float32 (T, E, 2) tensor on %s" % self.device)
+        T = actions.shape[0]
+        if tuple(actions.shape[1:]) != (self.E, 2) or actions.stride(2) != 1 or actions.stride(1) != 2:
+            raise ValueError("step_seq: actions (T, E, 2) with each step's (E, 2) rows contiguous required")
+        self.step_args()
+        with t.cuda.device(self.device):
+            _lib.check(_lib.lib().cn_step_seq(self._h, t.cuda.current_stream().cuda_stream, T, actions.data_ptr(),
+                                              actions.stride(0) if T > 1 else 2 * self.E, *self._step_args))
+        return self.obs(), self.reward, self.done, self.event, self.info, self.ep_return, self.ep_len
+
+    def step_args(self):
+        """The output pointers of step() / step_seq() (cached: the buffers are never reallocated)."""
+        if self._step_args is None:
+            self._step_fn = _lib.lib().cn_step
+            self._step_args = (self.robot_node.data_ptr(), self.temporal_edges.data_ptr(),
+                               self.spatial_edges.data_ptr(), self.reward.data_ptr(), self.done.data_ptr(),
+                               self.event.data_ptr(), self.info.data_ptr(), self.ep_return.data_ptr(),
+                               self.ep_len.data_ptr())
+        return self._step_args
 
     def set_graph_mode(self, on=True):
         """cn_set_graph_mode: keep the step sequence on the device so that step() can be captured in a

@@ -192,6 +192,16 @@ int cn_step(cn_engine *eng, void *stream, const float *actions,
             float *reward, uint8_t *done, int8_t *event, float *info,
             double *ep_return, int32_t *ep_len);
 
+/* T consecutive cn_step calls issued from native code: step t takes actions + t * action_stride
+ * (floats; >= 2 * E, e.g. a [T][E][2] tensor), the outputs are those of the last step (each step
+ * overwrites them, as T cn_step calls would). For open-loop action sequences (scripted or pre-drawn
+ * actions, bench.py's synthetic windows): the launches go back to back without a host round trip per
+ * step. Same kernels, same results as the T single calls. */
+int cn_step_seq(cn_engine *eng, void *stream, int T, const float *actions, int64_t action_stride,
+                float *robot_node, float *temporal_edges, float *spatial_edges,
+                float *reward, uint8_t *done, int8_t *event, float *info,
+                double *ep_return, int32_t *ep_len);
+
 /* State blob (layout: include/crowdnav_state.h). */
 /* Graph mode (on = 1): the step sequence (triple-buffered spawn-list indices, launch ids, the draw-all flag
  * after cn_reset / cn_set_state) moves from the host into device memory, so cn_step launches carry no

@@ -248,3 +248,40 @@ def test_sharded_gpu_equals_unsharded():
             assert torch.equal(of[k], torch.cat([o[0][k] for o in outs]))
         assert torch.equal(rf, torch.cat([o[1] for o in outs]))
         assert np.array_equal(df, np.concatenate([o[2] for o in outs]))
+
+
+@pytest.mark.gpu
+def test_step_seq_equals_single_steps():
+    """cn_step_seq (T launches issued from native code over a [T][E][2] action tensor) == T cn_step calls:
+    same state blob, same outputs of the last step, bit for bit (C2-like config incl. auto-resets and goal
+    changes: 64 envs x 10 humans, unicycle, 60 steps), for a plain and a mixed engine."""
+    from crowdnav_dsrnn_amd.config import make_mixed_cn_configs
+    from crowdnav_dsrnn_amd.engine import CrowdNavEngine
+
+    T, E = 60, 64
+    c = _config(10, "unicycle")
+    g = torch.Generator(device="cuda:0").manual_seed(7)
+    acts = (torch.rand((T, E, 2), generator=g, device="cuda:0") * 0.2 - 0.1).contiguous()
+    c5 = {s: _config(5, "holonomic", scen=(s,)) for s in ("parallel_traffic", "perpendicular_traffic")}
+    makers = [lambda: CrowdNavEngine(make_cn_config(c, num_envs=E, nenv=E, phase="train"), "cuda:0"),
+              lambda: CrowdNavEngine.mixed(*make_mixed_cn_configs(c5, list(c5), E, nenv=E, phase="train"),
+                                           device="cuda:0")]
+    for make in makers:
+        outs = []
+        for seq in (False, True):
+            eng = make()
+            eng.reset()
+            if seq:
+                o = eng.step_seq(acts)
+            else:
+                for t in range(T):
+                    o = eng.step(acts[t])
+            torch.cuda.synchronize()
+            st = eng.get_state()
+            blob = np.concatenate([v.blob.view(np.uint8).ravel() for _, v in st]) if isinstance(st, list) \
+                else np.asarray(st.blob).view(np.uint8)
+            outs.append([x.cpu().numpy().copy() for x in (o[0]["robot_node"], o[0]["spatial_edges"])] +
+                        [x.cpu().numpy().copy() for x in o[1:]] + [blob.copy()])
+            eng.close()
+        for a, b in zip(*outs):
+            np.testing.assert_array_equal(a, b)
