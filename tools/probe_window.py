@@ -51,6 +51,41 @@ for mode in ("seq", "host"):
             if pos > 2800:
                 pos = 5
             rows.append((mode, K, r % 2, (t2 - t0) * 1e6, (t1 - t0) * 1e6, e0.elapsed_time(e1) * 1e3))
+# bench.py's own bracket: reset count read, cn_profile armed (its two HIP events recorded by cn_step), barrier
+import ctypes  # noqa: E402
+
+from crowdnav_dsrnn_amd import _lib  # noqa: E402
+
+L = _lib.lib()
+for variant in ("bench", "bench_noprof", "bench_noreset"):
+    res = []
+    for r in range(reps):
+        K = 20
+        if variant != "bench_noreset":
+            bench.reset_total_dev(eng)
+        if variant != "bench_noprof":
+            _lib.check(L.cn_profile(eng._h, 1, K))
+        torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.step_seq(acts[pos:pos + K])
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        span = float("nan")
+        if variant != "bench_noprof":
+            a_ms, b_ms, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+            _lib.check(L.cn_profile_read(eng._h, ctypes.byref(a_ms), ctypes.byref(b_ms), ctypes.byref(n)))
+            _lib.check(L.cn_profile(eng._h, 0, 0))
+            span = a_ms.value * 1e3
+        pos += K
+        if pos > 2800:
+            pos = 5
+        res.append(((t2 - t0) * 1e6, (t1 - t0) * 1e6, span))
+    print("%-14s K=20: wall %s us, issue %s us, cn_profile span %s us" % (
+        variant, [round(x[0], 1) for x in res], [round(x[1], 1) for x in res], [round(x[2], 1) for x in res]),
+        flush=True)
 for mode in ("seq", "host"):
     for idle in (0, 1):
         sel = [x for x in rows if x[0] == mode and x[2] == idle]
