@@ -60,7 +60,10 @@ def main(steps=400, wl="c2", E=4096):
         R = r.reshape(-1, 2).astype(np.int64)
         live = np.nonzero(R[:, 1] > 0)[0]
         R = R[:live.max() + 1]
-        t0 = R[R[:, 0] > 0, 0].min()
+        # this launch's workgroups: stamps within 10 ms (100 MHz ticks) of its last end (entries of other
+        # launches or never written are older or zero)
+        fresh = R[:, 0] > R[:, 1].max() - 1000000
+        t0 = R[fresh, 0].min()
         en = (R[:, 1] - t0) * 10
         step_sel = np.zeros(len(R), bool)
         if wl == "c3":
