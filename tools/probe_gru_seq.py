@@ -67,6 +67,9 @@ def case(name, Bs, H, T=16, reps=3, F=0):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "pair":   # the edge-pair case alone (counter passes)
+        case("pair, x-mode", (20480, 2048), 256, F=64)
+        sys.exit(0)
     case("edge pair", (20480, 2048), 256)
     case("pair, x-mode", (20480, 2048), 256, F=64)
     case("spatial", (20480,), 256)
