@@ -3591,7 +3591,9 @@ __global__ void __launch_bounds__(64) cn_orca_kernel(int64_t n, int A, const flo
 // own ballot-partitioned walk; then the quad builds the ORCA lines in neighbour order and runs the quad
 // linear programs of the step kernel. Oracle: cpu_ref.c:kd_build / kd_query / rvo2_agent0.
 #define CN_ORCA_MAXA 64
-struct KdNodeS { int begin, end, left, right; float minX, maxX, minY, maxY; };
+// 20 B per node: ranges and child indices fit bytes (A <= 64 agents, < 2A nodes); the build / query stacks
+// below are bytes too -- the per-lane private arrays were 5.7 KB of scratch per lane with ints, 3.3 KB now
+struct KdNodeS { uint8_t begin, end, left, right; float minX, maxX, minY, maxY; };
 
 __device__ __forceinline__ float kd_bdist(const KdNodeS &t, float x, float y)
 {
@@ -3605,14 +3607,14 @@ __device__ __forceinline__ float kd_bdist(const KdNodeS &t, float x, float y)
 __device__ int kd_neighbors_seq(int A, const float *X, const float *Y, uint8_t *perm, float rangeSq, uint8_t *nb)
 {
     KdNodeS T[2 * CN_ORCA_MAXA];
-    int stk[CN_ORCA_MAXA + 2][3];
+    uint8_t stk[CN_ORCA_MAXA + 2][3];
     int sp = 0;
-    stk[sp][0] = 0; stk[sp][1] = A; stk[sp][2] = 0; ++sp;
+    stk[sp][0] = 0; stk[sp][1] = (uint8_t)A; stk[sp][2] = 0; ++sp;
     while (sp > 0) {   // any order of the recursive calls gives the same tree: children own disjoint ranges
         --sp;
         const int begin = stk[sp][0], end = stk[sp][1], node = stk[sp][2];
         KdNodeS t;
-        t.begin = begin; t.end = end; t.left = t.right = 0;
+        t.begin = (uint8_t)begin; t.end = (uint8_t)end; t.left = t.right = 0;
         t.minX = t.maxX = X[perm[begin]];
         t.minY = t.maxY = Y[perm[begin]];
         for (int i = begin + 1; i < end; ++i) {
@@ -3633,10 +3635,10 @@ __device__ int kd_neighbors_seq(int A, const float *X, const float *Y, uint8_t *
                 }
             }
             if (left == begin) { ++left; ++right; }
-            t.left = node + 1;
-            t.right = node + 2 * (left - begin);
-            stk[sp][0] = left; stk[sp][1] = end; stk[sp][2] = t.right; ++sp;
-            stk[sp][0] = begin; stk[sp][1] = left; stk[sp][2] = t.left; ++sp;
+            t.left = (uint8_t)(node + 1);
+            t.right = (uint8_t)(node + 2 * (left - begin));
+            stk[sp][0] = (uint8_t)left; stk[sp][1] = (uint8_t)end; stk[sp][2] = t.right; ++sp;
+            stk[sp][0] = (uint8_t)begin; stk[sp][1] = (uint8_t)left; stk[sp][2] = t.left; ++sp;
         }
         T[node] = t;
     }
@@ -3646,7 +3648,7 @@ __device__ int kd_neighbors_seq(int A, const float *X, const float *Y, uint8_t *
     float nd[CN_ORCA_MAXA];
     int cnt = 0;
     float dst[CN_ORCA_MAXA + 2];
-    int nst[CN_ORCA_MAXA + 2];
+    uint8_t nst[CN_ORCA_MAXA + 2];
     sp = 0;
     nst[0] = 0; dst[0] = -1.0f; sp = 1;
     const float x0 = X[0], y0 = Y[0];

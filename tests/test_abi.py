@@ -61,6 +61,22 @@ def test_gru_seq_rejects_bad_arguments_without_launching(L):
     assert L.cn_gru_bwd_seq(None, 0, 256, 1, bsegs, None) != 0     # T = 0
     assert L.cn_gru_bwd_seq(None, 4, 256, 1, bsegs, None) != 0
     assert b"cn_gru_bwd_seq" in L.cn_last_error()
+    # masked-state ring: nh >= 2 when T > 1 (a step reads hm[t % nh] while other workgroups write
+    # hm[(t + 1) % nh]); nh == T with save (the backward reads every step's hm). Rejected before any launch
+    # (non-null dummy addresses, 16-byte aligned, are never dereferenced)
+    seg = (_lib.GruSeqFwd * 1)()
+    seg[0] = _lib.GruSeqFwd(64, 16, 32, 48, 64, 80, 96, None, 1, None, None, None, 0)
+    assert L.cn_gru_fwd_seq(None, 4, 256, 1, seg) != 0 and b"nh >= 2" in L.cn_last_error()
+    seg[0].nh, seg[0].save = 2, 112
+    assert L.cn_gru_fwd_seq(None, 4, 256, 1, seg) != 0 and b"nh == T" in L.cn_last_error()
+
+
+def test_step_seq_and_graph_census_reject_bad_arguments(L):
+    """cn_step_seq / cn_graph_node_counts validate their arguments before touching the GPU."""
+    assert L.cn_step_seq(None, None, 4, None, 0, *([None] * 9)) != 0
+    counts = (ctypes.c_int64 * 4)()
+    assert L.cn_graph_node_counts(None, counts, 4, None) != 0
+    assert L.cn_graph_node_counts(ctypes.c_void_p(16), counts, 33, None) != 0   # n > 32
 
 
 def test_config_struct_size_matches(L):

@@ -71,3 +71,28 @@ def test_single_command_two_rank_launch_gloo(tmp_path):
     q = subprocess.run([sys.executable, os.path.join(os.path.dirname(bench.__file__), "bench.py"), "--gpus", "2",
                         "--dry-run"], env=env2, capture_output=True, text=True, timeout=120, cwd=str(tmp_path))
     assert q.returncode == 2 and "WORLD_SIZE" in q.stderr
+
+
+def test_window_object_arithmetic_and_fields():
+    """env_window_obj (the main window, steady_state and the side_c3 / side_c5 objects): value = all ranks'
+    env-steps / the window's max-over-ranks wall time, ms_per_step, the kernel time, resets, the wall-time
+    breakdown and the HBM roofline of the step kernel from the algorithmic bytes."""
+    m = {"workload": "c3", "W": 100, "K": 200, "launch": "cn_step_seq", "E_total": 4096, "N": 25,
+         "bpl": bench.algorithmic_bytes_per_env_step(25) * 4096,
+         "main": (0.11, 0.0005, 7219, 0.02)}
+    o = bench.env_window_obj(m, world=2)
+    assert o["value"] == round(2 * 4096 * 200 / 0.11, 1)
+    assert o["ms_per_step"] == round(0.11 / 200 * 1e3, 6) and o["step_kernel_ms"] == 0.5
+    assert o["launches"] == [100, 200] and o["resets"] == 7219 and o["window"] == "launches 101..300 after cn_reset"
+    assert o["window_ms"]["wall"] == 110.0 and o["window_ms"]["step_kernels"] == 100.0
+    r = o["roofline"]
+    assert r["bound"] == "hbm" and r["algorithmic_bytes_per_launch"] == 5274 * 4096
+    assert abs(r["achieved"] - 5274 * 4096 / 0.0005 / 1e9) < 1e-3 and r["peak"] == 8000.0
+
+
+def test_side_windows_are_the_survey_shapes():
+    """The default line's side windows: C3 and C5 after 100 warm-up launches over 200 timed ones, C4 one eager
+    update + the graph-capturing one, then 2 timed updates, all inside the watchdog's deadline."""
+    assert [w[0] for w in bench.SIDE_WINDOWS] == ["c3", "c5", "c4"]
+    assert dict((w[0], w[1:]) for w in bench.SIDE_WINDOWS) == {"c3": (100, 200), "c5": (100, 200), "c4": (2, 2)}
+    assert 0 < bench.SIDE_DEADLINE_S <= 300
