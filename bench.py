@@ -685,13 +685,21 @@ def main():
 
     import torch
 
+    # rehearsal knobs for the multi-rank path on a box with fewer GPUs than ranks (never set by the driver):
+    # CN_BENCH_SHARE_DEVICE=1 puts every rank on cuda:0, CN_BENCH_DIST_BACKEND=gloo replaces RCCL (which
+    # refuses two ranks on one GPU)
+    dev_index = 0 if os.environ.get("CN_BENCH_SHARE_DEVICE") == "1" else local_rank
+    backend = os.environ.get("CN_BENCH_DIST_BACKEND", "nccl")
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
+    device = torch.device("cuda", dev_index)
     torch.cuda.set_device(device)
 
     E, N, K, W = args.envs, args.humans, args.steps, args.warmup
