@@ -56,6 +56,9 @@ def algorithmic_bytes_per_env_step(N):
     return 2 * (112 + 96 * N) + 8 + 4 * (9 + 2 * N) + 4 + 2
 
 
+DIAG = None   # --diag (counter attribution runs only, never the line of record): "nogoal" = no goal changing
+
+
 def make_config(E, N, env_offset, nenv, workload="c2", rng="mt19937"):
     """SURVEY.md §8d workloads. c2 (default, the BASELINE metric): circle_crossing, ORCA, unicycle.
     c3: square_crossing ("random crossing"), robot/human FOV = pi, holonomic. c5: c5_mixed."""
@@ -64,6 +67,8 @@ def make_config(E, N, env_offset, nenv, workload="c2", rng="mt19937"):
     c = clone_config(Config())
     c.sim.human_num = N
     c.humans.policy = "orca"
+    if DIAG == "nogoal":
+        c.humans.random_goal_changing = c.humans.end_goal_changing = False
     if workload == "c3":
         c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
         c.action_space.kinematics = "holonomic"
@@ -198,6 +203,8 @@ def load_pmc(kernel="cn_step_kernel", workload="c2", window=None):
             continue
         wl = "c2"
         a = doc.get("bench_args", "").split()
+        if "--diag" in a:   # an attribution run of a modified workload: never reported
+            continue
         if "--workload" in a:
             wl = a[a.index("--workload") + 1]
         if wl != workload:
@@ -669,7 +676,10 @@ def main():
                     help="c2 = BASELINE metric (default); c3 / c4 / c5 are the SURVEY §8d side measurements "
                          "(c4: --steps / --warmup count PPO updates)")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--diag", choices=["nogoal"], default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    global DIAG
+    DIAG = args.diag
 
     kind, val = launch_plan(args.gpus, os.environ)
     if kind == "error":
@@ -735,7 +745,8 @@ def main():
             "dtype": "f64",
             "data": "synthetic",
             "config": {
-                "workload": WORKLOAD_DESC[args.workload] % (m["E_total"], N),
+                "workload": WORKLOAD_DESC[args.workload] % (m["E_total"], N) + (
+                    " [DIAGNOSTIC %s: not the metric's workload]" % DIAG if DIAG else ""),
                 "envs_per_gpu": m["E_total"], "humans": N if args.workload != "c5" else "5 (traffic) / 1 (side_pref)",
                 "global_envs": m["E_total"] * world,
                 "parallelism": "env-sharded x%d (no collective)" % world,
