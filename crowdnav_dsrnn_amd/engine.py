@@ -69,6 +69,7 @@ class CrowdNavEngine:
         self.ep_return = torch.zeros((E,), dtype=torch.float64, device=dev)
         self.ep_len = torch.zeros((E,), dtype=torch.int32, device=dev)
         self._step_args = None   # cached output pointers of step() (the buffers above are never reallocated)
+        self._seq_fn = None
 
     @classmethod
     def mixed(cls, cfgs, env_group, device=None):
@@ -120,10 +121,18 @@ class CrowdNavEngine:
         T = actions.shape[0]
         if tuple(actions.shape[1:]) != (self.E, 2) or actions.stride(2) != 1 or actions.stride(1) != 2:
             raise ValueError("step_seq: actions (T, E, 2) with each step's (E, 2) rows contiguous required")
-        self.step_args()
-        with t.cuda.device(self.device):
-            _lib.check(_lib.lib().cn_step_seq(self._h, t.cuda.current_stream().cuda_stream, T, actions.data_ptr(),
-                                              actions.stride(0) if T > 1 else 2 * self.E, *self._step_args))
+        if self._step_args is None:
+            self.step_args()
+        if self._seq_fn is None:
+            self._seq_fn = _lib.lib().cn_step_seq
+        stride = actions.stride(0) if T > 1 else 2 * self.E
+        if t.cuda.current_device() == self.device.index:
+            rc = self._seq_fn(self._h, t.cuda.current_stream().cuda_stream, T, actions.data_ptr(), stride, *self._step_args)
+        else:
+            with t.cuda.device(self.device):
+                rc = self._seq_fn(self._h, t.cuda.current_stream().cuda_stream, T, actions.data_ptr(), stride,
+                                  *self._step_args)
+        _lib.check(rc)
         return self.obs(), self.reward, self.done, self.event, self.info, self.ep_return, self.ep_len
 
     def step_args(self):
