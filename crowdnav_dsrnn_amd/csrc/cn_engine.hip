@@ -1441,12 +1441,94 @@ __device__ __forceinline__ bool disc_grid_hit(const DiscGrid &gr, const double *
     return hit;
 }
 
+// Cover of a crowded rejection loop's candidate box (kd-tree path, square_crossing: end goals in
+// goal_reject_crowded, spawn positions in wave_reject_discs): the box
+// [-hb, hb]^2 that holds every candidate (0.4 * rand_world_pt + noise, crowd_sim.py:313-318) in CN_GC x CN_GC
+// cells. Per row of cells, `cov` has bit i set where cell i lies inside ONE of the agents' position / goal
+// discs (so every try landing there is rejected); `arow` / `acol` are the agents whose discs' bounding boxes
+// overlap the row / column strip, so a try in an uncovered cell tests only the agents of arow & acol
+// exactly. Built per loop in one short pass (lane = row strip x half of the agents), unlike DiscGrid over the
+// discs' bounding box, whose ~0.45 m cells left ~30 % of the tries to the exact test (~2 % here).
+#define CN_GC 32
+struct GoalCover {
+    uint32_t *cov, *arow, *acol;   // [CN_GC] each
+    double *par;                   // x0 (= y0), CN_GC / (2 hb)
+};
+
+// Built in float32 with a 1e-4 m margin on both the cells (expanded) and the discs (shrunk for coverage,
+// grown for overlap), so no rounding of the build can mark a cell that the exact test (norm_lt, f64) would
+// not reject everywhere: a try is binned in float64 (at most ~1e-14 m off its cell), float32 coordinates
+// are ~1e-6 m off, and a cell can only be covered where the chord half-width w > s / 2 = 0.08 m, where
+// sqrtf is well conditioned.
+template <bool GOALS = true>
+__device__ __forceinline__ void goal_cover_build(const GoalCover &gc, const double *tx, const double *ty,
+                                                 const double *tgx, const double *tgy, const double *tmd, int NA,
+                                                 double hb, int lane)
+{
+    const double sd = 2 * hb / CN_GC;
+    const int r = lane & (CN_GC - 1), half = lane >> 5;
+    const float m = 1e-4f, x0 = (float)-hb, inv = (float)(CN_GC / (2 * hb));
+    const float s0 = (float)(-hb + r * sd) - m, s1 = (float)(-hb + (r + 1) * sd) + m;   // strip r, expanded
+    uint32_t cov = 0u, arow = 0u, acol = 0u;
+    for (int a = half; a < NA; a += 2) {
+        const float d = (float)tmd[a], dl = d + m, ds = d - m;
+#pragma unroll
+        for (int g = 0; g < (GOALS ? 2 : 1); ++g) {
+            const float cx = (float)(g ? tgx[a] : tx[a]), cy = (float)(g ? tgy[a] : ty[a]);
+            if (cy + dl >= s0 && cy - dl <= s1) arow |= 1u << a;
+            if (cx + dl >= s0 && cx - dl <= s1) acol |= 1u << a;
+            const float dy = fmaxf(fabsf(s0 - cy), fabsf(s1 - cy));   // farthest point of the strip in y
+            if (ds > dy) {
+                const float w = sqrtf(ds * ds - dy * dy);
+                // cells i with [x0 + i s - m, x0 + (i + 1) s + m] inside (cx - w, cx + w)
+                const int lo = max((int)floorf((cx - w - x0 + m) * inv) + 1, 0);
+                const int hi = min((int)floorf((cx + w - x0 - m) * inv) - 1, CN_GC - 1);
+                if (lo <= hi) cov |= (hi - lo == 31 ? ~0u : ((1u << (hi - lo + 1)) - 1u)) << lo;
+            }
+        }
+    }
+    cov |= __shfl_xor(cov, 32); arow |= __shfl_xor(arow, 32); acol |= __shfl_xor(acol, 32);
+    if (lane < CN_GC) { gc.cov[lane] = cov; gc.arow[lane] = arow; gc.acol[lane] = acol; }
+    if (lane == 0) { gc.par[0] = -hb; gc.par[1] = CN_GC / (2 * hb); }
+}
+
+// does the goal (gx, gy) lie strictly inside one of the agents' discs? Same answer as goal_hit over every
+// agent (GOALS = false: the position discs only, the spawn's placement test)
+template <bool GOALS = true>
+__device__ __forceinline__ bool goal_cover_hit(const GoalCover &gc, const double *tx, const double *ty,
+                                               const double *tgx, const double *tgy, const double *tmd, int NA,
+                                               double gx, double gy)
+{
+    const double fx = (gx - gc.par[0]) * gc.par[1], fy = (gy - gc.par[0]) * gc.par[1];
+    uint32_t msk;
+    if (fx >= 0.0 && fx < CN_GC && fy >= 0.0 && fy < CN_GC) {
+        const int ix = (int)fx, iy = (int)fy;
+        if ((gc.cov[iy] >> ix) & 1u) return true;
+        msk = gc.arow[iy] & gc.acol[ix];
+    } else msk = NA >= 32 ? ~0u : (1u << NA) - 1u;   // outside the box (not reached by its candidates)
+    bool hit = false;
+    while (msk && !hit) {
+        const int a0 = __ffs(msk) - 1;
+        msk &= msk - 1;
+        const int a1 = msk ? __ffs(msk) - 1 : a0;
+        msk &= msk - 1;
+        const double x0 = tx[a0], y0 = ty[a0], d0 = tmd[a0];
+        const double x1 = tx[a1], y1 = ty[a1], d1 = tmd[a1];
+        hit = norm_lt(gx - x0, gy - y0, d0) | norm_lt(gx - x1, gy - y1, d1);
+        if (GOALS) {
+            const double u0 = tgx[a0], v0 = tgy[a0], u1 = tgx[a1], v1 = tgy[a1];
+            hit = hit | norm_lt(gx - u0, gy - v0, d0) | norm_lt(gx - u1, gy - v1, d1);
+        }
+    }
+    return hit;
+}
+
 // wave_reject2 for "the candidate point (m.sl[t], m.sl[64 + t]) lies strictly inside one of NA discs"
 // (`disc(a, x, y, md)`: centre and radius of agent a): the spawn's human placement (crowd_sim.py:369-390).
 // When the wave has grid space (m.grid) the crowded passes bin the discs once into a DiscGrid (see
 // goal_reject_crowded) and test each try against its cell's agents only; same result.
 template <bool GRID, typename FC, typename FD>
-__device__ int wave_reject_discs(WRng &m, int W, int NA, int max_tries, uint32_t &ovf, FC cand, FD disc)
+__device__ int wave_reject_discs(WRng &m, int W, int NA, int max_tries, uint32_t &ovf, FC cand, FD disc, double hb = 0.0)
 {
     auto hit = [&](int t, int a) {
         double x, y, md;
@@ -1474,10 +1556,14 @@ __device__ int wave_reject_discs(WRng &m, int W, int NA, int max_tries, uint32_t
     }
     double *tx = (double *)m.grid, *ty = tx + 32, *tmd = tx + 64;
     DiscGrid gr;
+    GoalCover gc;
+    const bool cover = hb > 0.0 && NA <= 32;   // a candidate box: cover it (see GoalCover) instead of the discs' box
     gr.mask = (uint32_t *)(tx + 96); gr.cov = (uint64_t *)(tx + 96 + CN_GRID * CN_GRID / 2); gr.par = (double *)(gr.cov + 4);
+    gc.cov = (uint32_t *)(tx + 96); gc.arow = gc.cov + CN_GC; gc.acol = gc.arow + CN_GC; gc.par = (double *)(gc.acol + CN_GC);
     if (lane < NA) { double x, y, md; disc(lane, x, y, md); tx[lane] = x; ty[lane] = y; tmd[lane] = md; }
     wsync();
-    disc_grid_build<false>(gr, tx, ty, tx, ty, tmd, NA, lane);
+    if (cover) goal_cover_build<false>(gc, tx, ty, tx, ty, tmd, NA, hb, lane);
+    else disc_grid_build<false>(gr, tx, ty, tx, ty, tmd, NA, lane);
     const int J = min(64, CN_MT_N / W);
     for (;; t0 += J) {
         m.template ensure<true>(W * J);
@@ -1485,7 +1571,8 @@ __device__ int wave_reject_discs(WRng &m, int W, int NA, int max_tries, uint32_t
         const bool valid = lane < nt;
         if (valid) cand(m.p + W * lane, lane);
         wsync();
-        const bool bad = !valid || disc_grid_hit<false>(gr, tx, ty, tx, ty, tmd, m.sl[lane], m.sl[64 + lane]);
+        const bool bad = !valid || (cover ? goal_cover_hit<false>(gc, tx, ty, tx, ty, tmd, NA, m.sl[lane], m.sl[64 + lane])
+                                          : disc_grid_hit<false>(gr, tx, ty, tx, ty, tmd, m.sl[lane], m.sl[64 + lane]));
         const uint64_t okm = __ballot(!bad);
         if (okm) {
             const int first = __ffsll((long long)okm) - 1;
@@ -1507,10 +1594,11 @@ __device__ int wave_reject_discs(WRng &m, int W, int NA, int max_tries, uint32_t
 // GRID (the kd-tree path, whose waves have DiscGrid space in m.grid): the position and goal discs of the
 // agents are binned once per loop (disc_grid_build<true>) and each try tests only its cell's agents --
 // at 25 humans in square_crossing most of these loops run all max_tries = 1000 tries (16 passes), so the
-// one-off binning is repaid many times over; same result.
+// one-off binning is repaid many times over; same result. With a candidate box (hb > 0: square_crossing's
+// end goals) a GoalCover over the box replaces the DiscGrid.
 template <bool GRID, typename FC>
 __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, int self, double r_self, int W,
-                                   int max_tries, uint32_t &ovf, FC cand)
+                                   int max_tries, uint32_t &ovf, FC cand, double hb = 0.0)
 {
     const int lane = m.lane, NA = c.human_num;
     double *tx = m.sl + 128, *ty = tx + 32, *tgx = tx + 64, *tgy = tx + 96, *tmd = tx + 128;   // [32] each
@@ -1525,7 +1613,16 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
     }
     wsync();
     DiscGrid gr;
-    const bool grid = GRID && m.grid && NA >= 8;
+    GoalCover gc;
+    const bool cover = GRID && m.grid && NA >= 8 && NA <= 32 && hb > 0.0;
+    const bool grid = GRID && m.grid && NA >= 8 && !cover;
+    if (cover) {
+        gc.cov = (uint32_t *)(m.grid + 96 * 8);
+        gc.arow = gc.cov + CN_GC; gc.acol = gc.arow + CN_GC;
+        gc.par = (double *)(gc.acol + CN_GC);
+        goal_cover_build<true>(gc, tx, ty, tgx, tgy, tmd, NA, hb, lane);
+        wsync();
+    }
     if (grid) {
         gr.mask = (uint32_t *)(m.grid + 96 * 8);
         gr.cov = (uint64_t *)(m.grid + 96 * 8 + CN_GRID * CN_GRID * 4);
@@ -1553,7 +1650,8 @@ __device__ int goal_reject_crowded(const cn_config &c, const Env1 &en, WRng &m, 
         { const unsigned long long t_ = clock64(); tc_c += t_ - tq; tq = t_; }
 #endif
         bool bad = lane >= nt;
-        if (grid) bad = bad || disc_grid_hit<true>(gr, tx, ty, tgx, tgy, tmd, gx, gy);
+        if (cover) bad = bad || goal_cover_hit<true>(gc, tx, ty, tgx, tgy, tmd, NA, gx, gy);
+        else if (grid) bad = bad || disc_grid_hit<true>(gr, tx, ty, tgx, tgy, tmd, gx, gy);
         else
         for (int a0 = 0; a0 < NA && !bad; a0 += 4) {
             double x[4], y[4], u[4], v[4], d[4];
@@ -1675,7 +1773,7 @@ __device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64
                 ax = en.hpx[a - 1]; ay = en.hpy[a - 1];
                 md = rad + en.hr[a - 1] + c.discomfort_dist;
             }
-        });
+        }, sc == CN_SC_SQUARE_CROSSING ? 0.1 * c.square_width + 0.5 * fabs(vpref == 0 ? 1.0 : vpref) + 1e-3 : 0.0);
         if (lane == 0) {
             en.hpx[i] = m.sl[tw]; en.hpy[i] = m.sl[64 + tw]; en.hgx[i] = m.sl[128 + tw]; en.hgy[i] = m.sl[192 + tw];
             en.hth[i] = m.sl[256 + tw]; en.hvp[i] = m.sl[320 + tw]; en.hr[i] = rad;
@@ -1906,7 +2004,8 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
                         cand_attributes(c, m, q, sc, vpc, r_self, en.rr, px, py, gx, gy, hd, vp);
                     }
                     m.sl[tt] = gx; m.sl[64 + tt] = gy;
-                });
+                }, KIND == 1 && sc == CN_SC_SQUARE_CROSSING
+                       ? 0.1 * c.square_width + 0.5 * fabs(vpc == 0 ? 1.0 : vpc) + 1e-3 : 0.0);
                 if (lane == 0) { en.hgx[h] = m.sl[tw]; en.hgy[h] = m.sl[64 + tw]; }
                 wsync();
                 pg.pb = -(1 << 28);   // forces a rebuild before the next read
@@ -2013,7 +2112,8 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
 // spawn when `may_consume` and it is valid for the current key, else draw it here. One wave.
 template <bool GRID>
 __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2, const cn_config &c, int64_t E, int64_t e,
-                          int64_t counter_offset, bool may_consume, uint32_t launch_id, WRng &m, Env1 &en)
+                          int64_t counter_offset, bool may_consume, uint32_t launch_id, WRng &m, Env1 &en,
+                          uint32_t *inline_count = nullptr)
 {
     const cn_state_ptrs &S = o.s;
     const int N = c.human_num;
@@ -2047,6 +2147,7 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2,
         double rth;
         uint32_t ovf;
         int sc;
+        if (inline_count && lane == 0) atomicAdd(inline_count, 1u);
         spawn_env<GRID>(c, c.env_offset + orow(o.ov, e), cc, rc, counter_offset, m, en, rth, ovf, sc);
         const bool in1 = !m.phx && m.p > CN_MT_N;
         write_reset(o, c, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, lane);
@@ -2074,7 +2175,8 @@ struct PendLaunch {
     OutView ov;             // global env index = c.env_offset + orow(ov, e)
     long long budget;       // clock cycles a spawning wave works before parking (0: never parks)
     uint32_t launch_id;     // nonzero id of this launch (pending entries it completes carry it)
-    uint32_t *stats;        // [4] cumulative (kd-tree path): parked unstarted, parked mid-way, resumed, completed on resume
+    uint32_t *stats;        // [4] cumulative (kd-tree path): parked unstarted, parked mid-way, resumed, completed on
+                            // resume; [7] resets of the step workgroups that drew their spawn inline (every path)
 };
 
 // GRID: the spawn's crowded rejection through a DiscGrid (the kd-tree path's plans have LDS for it).
@@ -3217,7 +3319,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
                 const bool may = !g.pend.all;   // both pending slots are ready unless this launch draws all
-                reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m, en);
+                reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m, en, g.pend.stats + 7);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
                     const uint32_t k = atomicAdd(g.pcount_w, 1u);
                     if (k < (uint32_t)g.E) g.plist_w[k] = (uint32_t)e;
@@ -3477,7 +3579,7 @@ struct cn_engine {
     cn_state_ptrs s;
     uint32_t *work;       // [E]
     uint32_t *work_count; // [16]: [2..4] spawn-list counters (triple buffered), [5..7] parked-spawn counters,
-                          // [8..11] spawn statistics (PendLaunch::stats)
+                          // [8..11] spawn statistics (PendLaunch::stats), [15] inline reset draws
     uint32_t *plist;      // [3][E] envs whose next spawn kernel A draws
     uint32_t *rlist;      // [3][2E][4] spawns parked by a launch (resumed by the next); counters work_count[5..7]
     int devseq;           // graph mode (cn_set_graph_mode): the step sequence lives in work_count[12..14]
@@ -4339,18 +4441,19 @@ int cn_debug_set_spawn_budget(cn_engine *g, long long cycles)
 int cn_debug_spawn_stats(cn_engine *g, uint32_t *out)
 {
     if (!g || !out) return set_err(CN_EINVAL, "null argument");
-    for (int j = 0; j < 4; ++j) out[j] = 0;
+    for (int j = 0; j < 5; ++j) out[j] = 0;
     if (g->ngroups) {
         for (int k = 0; k < g->ngroups; ++k) {
-            uint32_t v[4];
+            uint32_t v[5];
             const int rc = cn_debug_spawn_stats(g->grp[k], v);
             if (rc) return rc;
-            for (int j = 0; j < 4; ++j) out[j] += v[j];
+            for (int j = 0; j < 5; ++j) out[j] += v[j];
         }
         return CN_OK;
     }
     HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(out, g->work_count + 8, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(out + 4, g->work_count + 15, sizeof(uint32_t), hipMemcpyDeviceToHost));
     return CN_OK;
 }
 

@@ -194,11 +194,12 @@ class CrowdNavEngine:
         _lib.check(_lib.lib().cn_debug_set_spawn_budget(self._h, int(cycles)))
 
     def spawn_stats(self):
-        """Cumulative kd-tree-path spawn counters (cn_debug_spawn_stats; synchronises): parked before
-        starting, parked mid-way, resumed, completed by a resume."""
-        out = (ctypes.c_uint32 * 4)()
+        """Cumulative spawn counters (cn_debug_spawn_stats; synchronises): kd-tree path spawns parked before
+        starting, parked mid-way, resumed, completed by a resume; auto-resets drawn inline (no pending spawn)."""
+        out = (ctypes.c_uint32 * 5)()
         _lib.check(_lib.lib().cn_debug_spawn_stats(self._h, out))
-        return dict(zip(("parked_unstarted", "parked_midway", "resumed", "completed_on_resume"), list(out)))
+        return dict(zip(("parked_unstarted", "parked_midway", "resumed", "completed_on_resume", "inline_resets"),
+                        list(out)))
 
     def close(self):
         if getattr(self, "_h", None) is not None:

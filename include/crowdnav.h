@@ -436,8 +436,9 @@ int cn_social_force_predict(void *stream, int64_t n, int M, const double *self, 
 /* Test hooks of the kd-tree path's resumable spawns (the spawn waves that draw upcoming episodes park a
  * crowded spawn between two humans once a wave has worked `cycles` clock cycles in a launch, and a later
  * launch resumes it; default 600000, 0 = never park; no effect on the quad path, which never parks).
- * cn_debug_spawn_stats: cumulative counts since cn_create [4] = spawns parked before they started, parked
- * mid-way, resumed, completed by a resume (synchronises the device). Results do not depend on the budget:
+ * cn_debug_spawn_stats: cumulative counts since cn_create [5] = spawns parked before they started, parked
+ * mid-way, resumed, completed by a resume (kd-tree path), and auto-resets whose spawn the step kernel drew
+ * inline because no pending spawn was ready (every path; synchronises the device). Results do not depend on the budget:
  * tests/test_gpu_parity.py forces parking after every human and compares with the oracle. */
 int cn_debug_set_spawn_budget(cn_engine *eng, long long cycles);
 int cn_debug_spawn_stats(cn_engine *eng, uint32_t *out);

@@ -32,13 +32,16 @@ def run(name, end_goal=True, rand_goal=True, E=4096, N=25, W=125, K=400):
     for s in range(W):
         eng.step(a[s])
     L = _lib.lib()
+    st0 = eng.spawn_stats()
     _lib.check(L.cn_profile(eng._h, 1, K))
     for s in range(K):
         eng.step(a[W + s])
     ta, tb, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
     _lib.check(L.cn_profile_read(eng._h, ctypes.byref(ta), ctypes.byref(tb), ctypes.byref(n)))
     us = ta.value * 1e3 / n.value
-    print("%-28s %8.1f us per launch  -> %.2f M env-steps/s" % (name, us, E / us), flush=True)
+    st1 = eng.spawn_stats()
+    print("%-28s %8.1f us per launch  -> %.2f M env-steps/s; per launch: %s" % (
+        name, us, E / us, ", ".join("%s %.1f" % (k, (st1[k] - st0[k]) / K) for k in st1)), flush=True)
     eng.close()
 
 
