@@ -1,7 +1,9 @@
+# A/B of C2 library variants, alternating: bash tools/ab_c2.sh OUTDIR lib1.so lib2.so ... (main window + steady state)
 set -o pipefail
-for k in 1 2 3; do
-timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/c2_head_$k.log 2>&1 || exit $?
-tail -1 gpurun_out/c2_head_$k.log | cut -c80-125
-CN_LIB_PATH=crowdnav_dsrnn_amd/lib/libcrowdnav_hip_k.so timeout -k 10 200 python -u bench.py --no-cpu-baseline > gpurun_out/c2_k_$k.log 2>&1 || exit $?
-tail -1 gpurun_out/c2_k_$k.log | cut -c80-125
-done
+O=$1; shift
+mkdir -p $O
+for r in 1 2; do for L in "$@"; do
+  n=$(basename $L .so)
+  CN_LIB_PATH=$L timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-side > $O/${n}_$r.log 2>&1 || exit $?
+  echo "$n: $(python tools/line_summary.py $O/${n}_$r.log | head -2 | tr '\n' ' ')"
+done; done

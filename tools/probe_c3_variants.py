@@ -46,6 +46,9 @@ def run(name, end_goal=True, rand_goal=True, E=4096, N=25, W=125, K=400):
 
 
 if __name__ == "__main__":
+    if sys.argv[1:] == ["default"]:
+        run("c3 (default) " + os.environ.get("CN_LIB_PATH", "").split("/")[-1])
+        sys.exit(0)
     run("c3 (default)")
     run("c3 no end-goal changes", end_goal=False)
     run("c3 no random goal changes", rand_goal=False)

@@ -19,6 +19,8 @@ from crowdnav_dsrnn_amd.engine import CrowdNavEngine  # noqa: E402
 
 
 def run(variant, E=4096, N=10, steps=300):
+    if variant.endswith("_301"):   # a last step that is not a multiple of 20 (random goal changes every 5 s)
+        variant, steps = variant[:-4], 301
     if variant == "c2w":   # the crowded circle centre of bench.py's --steps 20 --warmup 5 window
         steps = 16
     c = clone_config(Config())
@@ -161,6 +163,22 @@ def run(variant, E=4096, N=10, steps=300):
                     print("        %d rounds: %4d envs, cycles median %d max %d | walk %d first-tries %d reject-loop %d (mean)" % (
                         r, sel.sum(), np.median(part[sel]), part[sel].max(), goal[sel, k0].mean(), goal[sel, k0 + 1].mean(),
                         goal[sel, k0 + 2].mean()))
+    if len(goal) or len(res):   # the slowest 5 % workgroups' envs: what their RNG waves did (last step)
+        epb = 64 // N
+        slow_b = np.nonzero(slow)[0]
+        sel = np.zeros(E, bool)
+        for b in slow_b:
+            sel[b * epb:(b + 1) * epb] = True
+        rows = np.nonzero(cur)[0]
+        ss = rows[sel[rows]]
+        kinds = {"reset": ss[B[ss, 5] >= B[ss, 0]], "goal": ss[(B[ss, 4] >= B[ss, 0]) & (B[ss, 5] < B[ss, 0])]}
+        print("  slowest 5%% workgroups' envs (%d WGs, %d env items): resets %d, goal items %d" % (
+            len(slow_b), len(ss), len(kinds["reset"]), len(kinds["goal"])))
+        gi = kinds["goal"]
+        if len(gi):
+            gg = np.diff(B[gi, :5], axis=1)
+            print("    goal items: mt load %d random %d end %d write %d (mean); random changes mean %.2f, end changes mean %.2f" % (
+                *gg.mean(axis=0), ((B[gi, 6] % 1000) // 100).mean(), ((B[gi, 7] % 1000) // 100).mean()))
     if variant in ("c3", "c3nogoal"):
         L.cn_debug_stamps_c.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         cc = np.zeros(8192 * 4, np.uint64)
