@@ -96,6 +96,9 @@ struct StepPlan {
 #define CN_RENV_F 27   // robot/env doubles per env in LDS
 #define CN_HUM_F 14    // human doubles per lane in LDS
 #define CN_PEND_LDS (2 * CN_MT_N * 4 + 7 * 32 * 8 + 6 * 64 * 8)   // per RNG wave: MT ring, agent table, try slots
+#ifndef CN_COVER_RANDGOAL
+#define CN_COVER_RANDGOAL 1   // diagnostic switch: the candidate-box cover for random goals on the circle
+#endif
 #ifndef CN_RNG_PRIO_ALL
 #define CN_RNG_PRIO_ALL 0   // diagnostic: raise the RNG waves' priority on the quad path too
 #endif
@@ -1444,9 +1447,10 @@ __device__ __forceinline__ bool disc_grid_hit(const DiscGrid &gr, const double *
     return hit;
 }
 
-// Cover of a crowded rejection loop's candidate box (kd-tree path, square_crossing: end goals in
-// goal_reject_crowded, spawn positions in wave_reject_discs): the box
-// [-hb, hb]^2 that holds every candidate (0.4 * rand_world_pt + noise, crowd_sim.py:313-318) in CN_GC x CN_GC
+// Cover of a crowded rejection loop's candidate box (kd-tree path: square_crossing end goals and random goals
+// on the circle in goal_reject_crowded, square_crossing spawn positions in wave_reject_discs): the box
+// [-hb, hb]^2 that holds every candidate (0.4 * rand_world_pt + noise, crowd_sim.py:313-318; R cos / sin +
+// noise, :736-741) in CN_GC x CN_GC
 // cells. Per row of cells, `cov` has bit i set where cell i lies inside ONE of the agents' position / goal
 // discs (so every try landing there is rejected); `arow` / `acol` are the agents whose discs' bounding boxes
 // overlap the row / column strip, so a try in an uncovered cell tests only the agents of arow & acol
@@ -2007,8 +2011,8 @@ __device__ __forceinline__ int goal_pass(const cn_config &c, Env1 &en, WRng &m, 
                         cand_attributes(c, m, q, sc, vpc, r_self, en.rr, px, py, gx, gy, hd, vp);
                     }
                     m.sl[tt] = gx; m.sl[64 + tt] = gy;
-                }, KIND == 1 && sc == CN_SC_SQUARE_CROSSING
-                       ? 0.1 * c.square_width + 0.5 * fabs(vpc == 0 ? 1.0 : vpc) + 1e-3 : 0.0);
+                }, KIND == 0 ? (CN_COVER_RANDGOAL ? c.circle_radius + 0.5 * fabs(vpk) + 1e-3 : 0.0)
+                   : sc == CN_SC_SQUARE_CROSSING ? 0.1 * c.square_width + 0.5 * fabs(vpc == 0 ? 1.0 : vpc) + 1e-3 : 0.0);
                 if (lane == 0) { en.hgx[h] = m.sl[tw]; en.hgy[h] = m.sl[64 + tw]; }
                 wsync();
                 pg.pb = -(1 << 28);   // forces a rebuild before the next read
