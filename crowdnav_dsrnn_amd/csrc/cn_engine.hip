@@ -3281,8 +3281,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
         const bool done = sl.rflag[EPB + re] != 0;
         const bool rgoal = c.random_goal_changing && np_mod(gt, 5.0) == 0.0;
         const bool egoal = c.end_goal_changing && endg;
-        sl.rflag[EPB + re] = (done ? 1u : 0u) | (rgoal ? 2u : 0u) | (egoal ? 4u : 0u) |
-                              (pre_epl + 1 == 1 ? 8u : 0u);
+        sl.rflag[EPB + re] = (done ? 1u : 0u) | (rgoal ? 2u : 0u) | (egoal ? 4u : 0u);
     }
     __syncthreads();
     STAMP_A(4);
@@ -3290,8 +3289,8 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
 
     // ---- phase 5: this workgroup's RNG work, one wave per env needing it --------------------------
     // Done envs auto-reset (VecEnv worker, shmem_vec_env.py:164-168) from the pending spawn drawn by an
-    // earlier launch; an env reset by the previous launch (ep_len == 1) may be redrawn by this launch's
-    // spawn waves right now, so it (and every env after cn_reset/cn_set_state) draws inline instead.
+    // earlier launch (reset_env: two slots per env, consumed only when an earlier launch completed the entry);
+    // after cn_reset / cn_set_state, while this launch's spawn waves draw every env's entries, they draw inline.
     {
         // the wave index is wave-uniform: readfirstlane keeps it (and every LDS pointer derived from it) in
         // SGPRs -- as a VGPR value the RNG block's preheader spilled it to scratch (HBM writes every launch)
