@@ -1109,6 +1109,14 @@ struct ResetOut {
     OutView ov;
 };
 
+// pending-spawn modes of a step launch (PendLaunch::all): after cn_set_state every env's next spawn and the one
+// after are drawn (resets of that launch draw inline); after cn_reset the reset kernel drew both (ok word
+// CN_OK_RESET, never a step launch's id) and the launch draws none -- both modes ignore the spawn and resume
+// lists of launches before them
+#define PEND_BOTH 1
+#define PEND_FRESH 2
+#define CN_OK_RESET 0xffffffffu
+
 struct RngArgs {   // cn_reset_kernel
     ResetOut o;
     PendPtrs pend;
@@ -2172,7 +2180,7 @@ struct PendLaunch {
     const uint32_t *rcount;
     uint32_t *rlist_w;      // spawns this launch parks
     uint32_t *rcount_w;
-    int all;                // 1: every env (list ignored)
+    int all;                // PEND_BOTH: every env's two spawns, PEND_FRESH: none (lists ignored); 0: the lists
     int step_blocks, pend_blocks;
     int first;              // 1: workgroups [0, pend_blocks) (kd-tree path); 0: after the step workgroups
     int waves;              // spawning waves per spare workgroup (RNG regions that fit the launch's LDS)
@@ -2203,7 +2211,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
     double *hb = (double *)(base + 2 * CN_MT_N * 4);
     // envs reset by the previous launch: the reset after next (the next one was drawn earlier); after
     // cn_reset / cn_set_state (all): both the next (items [0, E)) and the one after ([E, 2E))
-    const uint32_t nnew = pl.all ? (uint32_t)(2 * E) : min(*pl.count, (uint32_t)E);
+    const uint32_t nnew = pl.all == PEND_BOTH ? (uint32_t)(2 * E) : pl.all ? 0u : min(*pl.count, (uint32_t)E);
     // parking / resuming exists on the kd-tree path only (GRID): the quad path's spawns are short, and
     // its kernel keeps the plain loop (register pressure of the step path)
     const uint32_t nres = (!GRID || pl.all) ? 0u : min(*pl.rcount, (uint32_t)(2 * E));
@@ -2216,7 +2224,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         bool started = false;
         if (it < nnew) {
             e = pl.all ? (int64_t)(it % (uint32_t)E) : (int64_t)pl.list[it];
-            const bool ahead2 = !pl.all || it >= (uint32_t)E;
+            const bool ahead2 = pl.all != PEND_BOTH || it >= (uint32_t)E;
             cc = S.case_counter[e];
             rc = S.reset_count[e];
             if (ahead2) { cc = (cc + c.nenv) % pl.case_size; rc += 1; }   // write_reset's counter update
@@ -2386,7 +2394,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
         g.pend.rlist_w = g.rlist_base + kw * rs;
         g.pend.rcount_w = g.ctl + 5 + kw;
         g.pend.launch_id = ((ns + 1u) % 0x7ffffffeu) + 1u;   // nonzero, differs from the neighbours'
-        g.pend.all = g.ctl[CN_CTL_ALL] != 0u;
+        g.pend.all = (int)g.ctl[CN_CTL_ALL];
     }
     // the last workgroup to finish advances the sequence (every workgroup has read it by then)
     // (the atomic carries a register dependency on this workgroup's read of the counter, so the read has
@@ -3327,7 +3335,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             if (need & 1u) {
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
-                const bool may = !g.pend.all;   // both pending slots are ready unless this launch draws all
+                const bool may = g.pend.all != PEND_BOTH;   // the slots are ready unless this launch redraws both
                 reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m, en, g.pend.stats + 7);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
                     const uint32_t k = atomicAdd(g.pcount_w, 1u);
@@ -3371,6 +3379,22 @@ __global__ void __launch_bounds__(64) cn_reset_kernel(RngArgs g, cn_config c)
         m.w = mtw; m.off = 0; m.lane = lane; m.sl = slots; m.phx = c.rng_mode == CN_RNG_PHILOX; m.edbg = -1;
         m.grid = gridbuf;
         reset_env<true>(g.o, g.pend, c, g.E, e, g.counter_offset, true, 0u, m, en);
+        // and the spawns of the env's next two resets (both pending slots), so that the first step launches
+        // find every spawn they need drawn (PEND_FRESH): keys = the counters the reset just wrote, advanced
+        int64_t cc1 = g.o.s.case_counter[e];
+        int32_t rc1 = g.o.s.reset_count[e];
+        for (int k = 0; k < 2; ++k) {
+            double rth;
+            uint32_t ovf;
+            int sc;
+            spawn_env<true>(c, c.env_offset + orow(g.o.ov, e), cc1, rc1, g.counter_offset, m, en, rth, ovf, sc);
+            const bool in1 = !m.phx && m.p > CN_MT_N;
+            write_pending<true>(g.pend, c, g.E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc1,
+                                rc1, lane, CN_OK_RESET, c.human_num);
+            wsync();
+            cc1 = (cc1 + c.nenv) % g.o.case_size;   // write_reset's counter update
+            rc1 += 1;
+        }
     }
 }
 
@@ -3593,7 +3617,7 @@ struct cn_engine {
     uint32_t *rlist;      // [3][2E][4] spawns parked by a launch (resumed by the next); counters work_count[5..7]
     int devseq;           // graph mode (cn_set_graph_mode): the step sequence lives in work_count[12..14]
     uint32_t ctl_host[4];
-    int pend_all;         // next kernel A draws every env's spawn (after cn_reset / cn_set_state)
+    int pend_all;         // next kernel A's pending mode: PEND_BOTH (after cn_set_state) or PEND_FRESH (after cn_reset)
     uint64_t nstep;
     long long spawn_budget;   // clock cycles a spawning wave works per launch before parking (0: never)
     void *pend_mem;       // pending next-episode spawns (PendPtrs)
@@ -4020,7 +4044,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         g->pend.r = (double *)b; b += pb_r;
         g->pend.h = (double *)b;
     }
-    g->pend_all = 1;
+    g->pend_all = PEND_BOTH;
     {
         // the plan holds phase 5's RNG regions (laid over the ORCA scratch); spare workgroups run as many
         // spawning waves as regions fit in the same allocation
@@ -4238,10 +4262,10 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_reset_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
     HIPCHK(hipGetLastError());
-    // every env starts a new episode: the next step launch draws all next spawns (host flag; graph mode: the
-    // device flag, stream-ordered)
-    g->pend_all = 1;
-    if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, 1u, st);
+    // every env starts a new episode with its next two spawns drawn: the next step launch draws none and
+    // ignores the earlier launches' lists (host flag; graph mode: the device flag, stream-ordered)
+    g->pend_all = PEND_FRESH;
+    if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, PEND_FRESH, st);
     return CN_OK;
 }
 
@@ -4347,7 +4371,7 @@ int cn_set_graph_mode(cn_engine *g, void *stream, int on)
     } else if (!on && g->devseq) {   // and back
         HIPCHK(hipMemcpyAsync(g->ctl_host, g->work_count + CN_CTL_NSTEP, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        g->nstep = g->ctl_host[0]; g->pend_all = g->ctl_host[1] ? 1 : 0;
+        g->nstep = g->ctl_host[0]; g->pend_all = (int)g->ctl_host[1];
     }
     g->devseq = on ? 1 : 0;
     return CN_OK;
@@ -4404,8 +4428,8 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
         HIPCHK(hipMemcpyAsync(g->state, src, g->state_bytes, hipMemcpyDeviceToDevice, st));
     }
     // pending spawns are keyed by (case_counter, reset_count); redraw them for the new state
-    g->pend_all = 1;
-    if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, 1u, st);
+    g->pend_all = PEND_BOTH;
+    if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, PEND_BOTH, st);
     return CN_OK;
 }
 

@@ -254,7 +254,8 @@ def test_gpu_forced_spawn_parking_matches_oracle(gpu, oracle):
         errs = H.compare_state(gs, d, "post_", tol=1e-5)
         assert not errs, errs
         st = g.eng.spawn_stats()
-        assert st["parked_midway"] > 1000 and st["resumed"] > 1000 and st["completed_on_resume"] > 50, (rngmode, st)
+        # (cn_reset draws every env's next two spawns itself, so the spawn waves' work starts at the third)
+        assert st["parked_midway"] > 1000 and st["resumed"] > 1000 and st["completed_on_resume"] > 25, (rngmode, st)
 
 
 def test_gpu_full_size_c3_free_running(gpu, oracle):

@@ -51,6 +51,7 @@ def main(steps=400, wl="c2", E=4096):
     ta, tb, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
     rows = []
     prev_done = E   # cn_reset: every env's first spawn was drawn by the reset kernel, the next ones ahead
+    st_prev = eng.spawn_stats()
     for s in range(steps):
         r[:] = 0
         _lib.check(L.cn_profile(eng._h, 1, 1))
@@ -71,14 +72,17 @@ def main(steps=400, wl="c2", E=4096):
         else:
             step_sel[:blocks] = True
         d = int(eng.done.sum().item())
+        st = eng.spawn_stats()
         rows.append((ta.value * 1e3, en[step_sel].max(), en[~step_sel].max() if (~step_sel).any() else 0,
-                     np.percentile(en[step_sel], 50), prev_done))
+                     np.percentile(en[step_sel], 50), prev_done, st["inline_resets"] - st_prev["inline_resets"],
+                     st["parked_unstarted"] - st_prev["parked_unstarted"] + st["parked_midway"] - st_prev["parked_midway"]))
+        st_prev = st
         prev_done = d
     _lib.check(L.cn_profile(eng._h, 0, 0))
     # spawn_env segments (the latest spawn of each env: seeding, robot, humans 0..N-1), cycles
     Sg = sp.reshape(-1, 16).astype(np.int64)[:E]
-    ok = Sg[:, 3 + N - 1] > Sg[:, 0]
-    if ok.any():
+    ok = Sg[:, min(3 + N - 1, 15)] > Sg[:, 0]
+    if ok.any() and 3 + N <= 16:   # segments of up to 13 humans are stamped
         Sg = Sg[ok]
         seg = np.diff(Sg[:, :3 + N], axis=1)
         print("[%s] spawn_env segments over %d envs' latest spawn (cycles, median / p90): seed %d / %d, robot %d / %d, "
@@ -89,9 +93,10 @@ def main(steps=400, wl="c2", E=4096):
                   np.percentile(Sg[:, 2 + N] - Sg[:, 0], 90)))
     a = np.asarray(rows)
     print("[%s] launch | kernel us | last step-WG end us | last spawn-WG end us | median step-WG end | "
-          "resets drawn ahead (prev done)" % wl)
+          "resets drawn ahead (prev done) | resets drawn inline | spawns parked" % wl)
     for s in range(min(30, steps)):
-        print("  %4d  %7.1f  %7.1f  %7.1f  %7.1f  %5d" % (s, a[s, 0], a[s, 1] / 1e3, a[s, 2] / 1e3, a[s, 3] / 1e3, a[s, 4]))
+        print("  %4d  %7.1f  %7.1f  %7.1f  %7.1f  %5d  %5d  %5d" % (s, a[s, 0], a[s, 1] / 1e3, a[s, 2] / 1e3, a[s, 3] / 1e3,
+                                                           a[s, 4], a[s, 5], a[s, 6]))
     rest = a[30:]
     if len(rest):
         spawn_last = (rest[:, 2] > rest[:, 1]).mean()
