@@ -1122,6 +1122,7 @@ struct RngArgs {   // cn_reset_kernel
     PendPtrs pend;
     int E;
     int64_t counter_offset;
+    int draw_next;   // also draw the spawns of every env's next two resets (kd-tree path: PEND_FRESH)
 };
 
 
@@ -2211,7 +2212,8 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
     double *hb = (double *)(base + 2 * CN_MT_N * 4);
     // envs reset by the previous launch: the reset after next (the next one was drawn earlier); after
     // cn_reset / cn_set_state (all): both the next (items [0, E)) and the one after ([E, 2E))
-    const uint32_t nnew = pl.all == PEND_BOTH ? (uint32_t)(2 * E) : pl.all ? 0u : min(*pl.count, (uint32_t)E);
+    // (the quad path never sees PEND_FRESH: cn_reset's kernel pre-draws on the kd-tree path only)
+    const uint32_t nnew = (!GRID || pl.all == PEND_BOTH) && pl.all ? (uint32_t)(2 * E) : pl.all ? 0u : min(*pl.count, (uint32_t)E);
     // parking / resuming exists on the kd-tree path only (GRID): the quad path's spawns are short, and
     // its kernel keeps the plain loop (register pressure of the step path)
     const uint32_t nres = (!GRID || pl.all) ? 0u : min(*pl.rcount, (uint32_t)(2 * E));
@@ -2224,7 +2226,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         bool started = false;
         if (it < nnew) {
             e = pl.all ? (int64_t)(it % (uint32_t)E) : (int64_t)pl.list[it];
-            const bool ahead2 = pl.all != PEND_BOTH || it >= (uint32_t)E;
+            const bool ahead2 = (GRID ? pl.all != PEND_BOTH : !pl.all) || it >= (uint32_t)E;
             cc = S.case_counter[e];
             rc = S.reset_count[e];
             if (ahead2) { cc = (cc + c.nenv) % pl.case_size; rc += 1; }   // write_reset's counter update
@@ -3335,7 +3337,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             if (need & 1u) {
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
-                const bool may = g.pend.all != PEND_BOTH;   // the slots are ready unless this launch redraws both
+                const bool may = KD ? g.pend.all != PEND_BOTH : !g.pend.all;   // ready unless this launch redraws both
                 reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m, en, g.pend.stats + 7);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
                     const uint32_t k = atomicAdd(g.pcount_w, 1u);
@@ -3383,7 +3385,7 @@ __global__ void __launch_bounds__(64) cn_reset_kernel(RngArgs g, cn_config c)
         // find every spawn they need drawn (PEND_FRESH): keys = the counters the reset just wrote, advanced
         int64_t cc1 = g.o.s.case_counter[e];
         int32_t rc1 = g.o.s.reset_count[e];
-        for (int k = 0; k < 2; ++k) {
+        for (int k = 0; k < (g.draw_next ? 2 : 0); ++k) {
             double rth;
             uint32_t ovf;
             int sc;
@@ -4259,13 +4261,18 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     a.o.case_size = g->case_size;
     a.o.ov.row = g->rows; a.o.ov.NS = g->NS;
     a.pend = g->pend; a.E = g->E; a.counter_offset = g->counter_offset;
+    // kd-tree path: the reset kernel draws the next two spawns too, so the first step launches (whose crowded
+    // spawns would otherwise run inline in step workgroups until the spawn waves catch up) find them drawn;
+    // the quad path's spawns are short and its first launch draws them (PEND_BOTH, as after cn_set_state)
+    a.draw_next = g->plan.kd ? 1 : 0;
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_reset_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
     HIPCHK(hipGetLastError());
-    // every env starts a new episode with its next two spawns drawn: the next step launch draws none and
-    // ignores the earlier launches' lists (host flag; graph mode: the device flag, stream-ordered)
-    g->pend_all = PEND_FRESH;
-    if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, PEND_FRESH, st);
+    // every env starts a new episode (kd-tree path: with its next two spawns drawn): the next step launch
+    // draws them (none) and ignores the earlier launches' lists (host flag; graph mode: the device flag,
+    // stream-ordered)
+    g->pend_all = a.draw_next ? PEND_FRESH : PEND_BOTH;
+    if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, (uint32_t)g->pend_all, st);
     return CN_OK;
 }
 
