@@ -285,3 +285,45 @@ def test_step_seq_equals_single_steps():
             eng.close()
         for a, b in zip(*outs):
             np.testing.assert_array_equal(a, b)
+
+
+def _c3_engine(E):
+    from crowdnav_dsrnn_amd.engine import CrowdNavEngine
+
+    c = clone_config(Config())
+    c.sim.human_num = 25
+    c.humans.policy = "orca"
+    c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
+    c.action_space.kinematics = "holonomic"
+    c.robot.FOV = c.humans.FOV = 1.0
+    return CrowdNavEngine(make_cn_config(c, num_envs=E, nenv=E, phase="train"), "cuda:0")
+
+
+@pytest.mark.gpu
+def test_c3_first_launches_find_their_spawns_and_runs_repeat():
+    """The kd-tree path after cn_reset (C3 shape, 1024 envs x 25 humans, 60 launches): the reset kernel draws
+    every env's next two spawns, so no reset of the first launches draws a crowded spawn inline; and two runs
+    from the same reset and actions (spawns parked and resumed at run-dependent points in between) end in the
+    same state bit for bit, with different spawn budgets too (results never depend on the parking)."""
+    E, T = 1024, 60
+    g = torch.Generator(device="cuda:0").manual_seed(11)
+    acts = (torch.randn((T, E, 2), generator=g, device="cuda:0") * 0.5).contiguous()
+    blobs = []
+    for budget in (None, None, 20000):
+        eng = _c3_engine(E)
+        if budget is not None:
+            eng.set_spawn_budget(budget)
+        eng.reset()
+        st0 = eng.spawn_stats()
+        resets = 0
+        for t in range(T):
+            eng.step(acts[t])
+            resets += int(eng.done.sum().item())
+        st = eng.spawn_stats()
+        assert resets > 0
+        if budget is None:
+            assert st["inline_resets"] - st0["inline_resets"] == 0, st
+        blobs.append(np.asarray(eng.get_state().blob).copy())
+        eng.close()
+    np.testing.assert_array_equal(blobs[0], blobs[1])
+    np.testing.assert_array_equal(blobs[0], blobs[2])
