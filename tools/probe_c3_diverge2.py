@@ -2,7 +2,7 @@
 every later run compares at the same launches and, at the first difference, prints the launch, the envs and
 the differing fields with both runs' values for the first envs.
 
-    python tools/probe_c3_diverge2.py [R] [K] [S]
+    python tools/probe_c3_diverge2.py [R] [K] [S] [spawn budget]
 """
 import os
 import sys
@@ -26,10 +26,12 @@ def make(E=4096, N=25):
     return CrowdNavEngine(make_cn_config(c, num_envs=E, nenv=E, phase="train"), "cuda:0"), E, N
 
 
-def main(R=12, K=400, S=10):
+def main(R=12, K=400, S=10, budget=None):
     ref = []
     for r in range(R):
         eng, E, N = make()
+        if budget is not None:
+            eng.set_spawn_budget(budget)
         g = torch.Generator(device="cuda:0")
         g.manual_seed(0)
         eng.reset()
@@ -70,4 +72,4 @@ def main(R=12, K=400, S=10):
 
 
 if __name__ == "__main__":
-    main(*(int(x) for x in sys.argv[1:4]))
+    main(*(int(x) for x in sys.argv[1:5]))
