@@ -25,6 +25,8 @@ def run(name, end_goal=True, rand_goal=True, E=4096, N=25, W=125, K=400):
     c.humans.end_goal_changing = end_goal
     c.humans.random_goal_changing = rand_goal
     eng = CrowdNavEngine(make_cn_config(c, num_envs=E, nenv=E, phase="train"), "cuda:0")
+    if os.environ.get("CN_SPAWN_BUDGET"):
+        eng.set_spawn_budget(int(os.environ["CN_SPAWN_BUDGET"]))
     g = torch.Generator(device="cuda:0")
     g.manual_seed(0)
     a = torch.randn((W + K, E, 2), generator=g, device="cuda:0") * 0.5
