@@ -4060,10 +4060,13 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         const int cap = (g->plan.kd ? 256 : 128) / nw;
         const int pb = (int)(need < cap ? need : cap);
         g->pend_blocks = g->plan.kd ? (pb + 7) & ~7 : pb;   // leading: a multiple of 8 (XCD placement)
-        // kd-tree path: a crowded spawn (~1M cycles) may take longer than the launch's step rounds; each
-        // spawning wave parks its spawn after ~0.6M cycles and a later launch resumes it (the spawn is
-        // needed one whole episode later). The quad path's spawns are short: never parked.
-        g->spawn_budget = g->plan.kd ? 600000 : 0;
+        // kd-tree path: a crowded spawn may take longer than the launch's step rounds; with a budget each
+        // spawning wave parks its spawn after that many cycles and a later launch resumes it (the spawn is
+        // needed one whole episode later). Off by default since round 5: with parking on (600 k cycles), 5 of
+        // 149 C3 runs of 400 launches departed from the others in one env (a spawn's last humans), 0 of 208
+        // without; since the candidate-box covers made crowded spawns ~2.3x cheaper, parking is worth only
+        // 1.7 % of C3 steady state (423 vs 430 us). The quad path's spawns are short: never parked.
+        g->spawn_budget = 0;
     }
     cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
     if (circ_table_init() != hipSuccess) {
