@@ -2175,7 +2175,7 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2,
 // (or of every env after cn_reset / cn_set_state). One wave per env, independent of the other waves.
 struct PendLaunch {
     PendPtrs P;
-    const uint32_t *list;   // envs reset by the previous launch
+    const uint32_t *list;   // envs reset by the previous launch: {e, reset_count, case_counter lo, hi} after it
     const uint32_t *count;
     const uint32_t *rlist;  // spawns parked by the previous launch: {e | 2^31 if not started, key rc, cc lo, cc hi}
     const uint32_t *rcount;
@@ -2225,10 +2225,17 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         int32_t rc;
         bool started = false;
         if (it < nnew) {
-            e = pl.all ? (int64_t)(it % (uint32_t)E) : (int64_t)pl.list[it];
             const bool ahead2 = (GRID ? pl.all != PEND_BOTH : !pl.all) || it >= (uint32_t)E;
-            cc = S.case_counter[e];
-            rc = S.reset_count[e];
+            if (pl.all) {   // cn_set_state: the state's counters (no step launch is rewriting them)
+                e = (int64_t)(it % (uint32_t)E);
+                cc = S.case_counter[e];
+                rc = S.reset_count[e];
+            } else {        // the counters the previous launch's reset wrote (carried by the list entry)
+                const uint32_t *q = pl.list + 4 * it;
+                e = (int64_t)q[0];
+                rc = (int32_t)q[1];
+                cc = (int64_t)((uint64_t)q[2] | ((uint64_t)q[3] << 32));
+            }
             if (ahead2) { cc = (cc + c.nenv) % pl.case_size; rc += 1; }   // write_reset's counter update
         } else {
             const uint32_t *q = pl.rlist + 4 * (it - nnew);
@@ -2325,7 +2332,7 @@ struct StepArgs {
     // has no per-call arguments and a sequence of cn_step calls can be captured in a hipGraph and replayed;
     // the pointers below are then derived at the top of the kernel. Otherwise the host passes them.
     uint32_t *ctl;
-    uint32_t *plist_base;   // [3][E + 64] spawn lists
+    uint32_t *plist_base;   // [3][E + 64][4] spawn lists: {env, reset_count, case_counter lo, hi} after the reset
     uint32_t *rlist_base;   // [3][2E + 64][4] parked-spawn lists
     uint32_t *plist_w;      // envs reset by this launch (their next spawn is drawn by the next launch)
     uint32_t *pcount_w;
@@ -2384,7 +2391,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
     const uint32_t ns = DEVSEQ ? g.ctl[CN_CTL_NSTEP] : 0u;
     if (DEVSEQ) {
         const int64_t kw = ns % 3u, kr = (ns + 2u) % 3u, kz = (ns + 1u) % 3u;
-        const int64_t ls = (int64_t)g.E + 64, rs = 4 * (2 * (int64_t)g.E + 64);
+        const int64_t ls = 4 * ((int64_t)g.E + 64), rs = 4 * (2 * (int64_t)g.E + 64);
         g.plist_w = g.plist_base + kw * ls;
         g.pcount_w = g.ctl + 2 + kw;
         g.pcount_zero = g.ctl + 2 + kz;
@@ -3340,8 +3347,17 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                 const bool may = KD ? g.pend.all != PEND_BOTH : !g.pend.all;   // ready unless this launch redraws both
                 reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m, en, g.pend.stats + 7);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
+                    // the entry carries the counters this reset just wrote (its own stores, read back), so the
+                    // next launch's spawn wave keys the spawn after next from them, never from a state that a
+                    // later reset of the same env may be rewriting while it reads
+                    const int64_t ccn = S.case_counter[e];
+                    const int32_t rcn = S.reset_count[e];
                     const uint32_t k = atomicAdd(g.pcount_w, 1u);
-                    if (k < (uint32_t)g.E) g.plist_w[k] = (uint32_t)e;
+                    if (k < (uint32_t)g.E) {
+                        uint32_t *q = g.plist_w + 4 * k;
+                        q[0] = (uint32_t)e; q[1] = (uint32_t)rcn;
+                        q[2] = (uint32_t)(uint64_t)ccn; q[3] = (uint32_t)((uint64_t)ccn >> 32);
+                    }
                 }
                 STAMP_B(e, 5);
             } else {
@@ -3615,7 +3631,7 @@ struct cn_engine {
     uint32_t *work;       // [E]
     uint32_t *work_count; // [16]: [2..4] spawn-list counters (triple buffered), [5..7] parked-spawn counters,
                           // [8..11] spawn statistics (PendLaunch::stats), [15] inline reset draws
-    uint32_t *plist;      // [3][E] envs whose next spawn kernel A draws
+    uint32_t *plist;      // [3][E + 64][4] envs whose spawn after next kernel A draws, with their counters
     uint32_t *rlist;      // [3][2E][4] spawns parked by a launch (resumed by the next); counters work_count[5..7]
     int devseq;           // graph mode (cn_set_graph_mode): the step sequence lives in work_count[12..14]
     uint32_t ctl_host[4];
@@ -4018,7 +4034,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     hipError_t e1 = hipMalloc(&g->state, g->state_bytes);
     hipError_t e2 = hipMalloc(&g->work, sizeof(uint32_t) * (g->E + 64));
     hipError_t e3 = hipMalloc(&g->work_count, 64);
-    hipError_t e4 = hipMalloc(&g->plist, sizeof(uint32_t) * 3 * (g->E + 64));
+    hipError_t e4 = hipMalloc(&g->plist, sizeof(uint32_t) * 3 * 4 * (g->E + 64));
     hipError_t e6 = hipMalloc(&g->rlist, sizeof(uint32_t) * 3 * 4 * (2 * (int64_t)g->E + 64));
     hipError_t e5 = hipMalloc(&g->pend_mem, pend_bytes);
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess || e4 != hipSuccess || e5 != hipSuccess ||
@@ -4060,13 +4076,13 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         const int cap = (g->plan.kd ? 256 : 128) / nw;
         const int pb = (int)(need < cap ? need : cap);
         g->pend_blocks = g->plan.kd ? (pb + 7) & ~7 : pb;   // leading: a multiple of 8 (XCD placement)
-        // kd-tree path: a crowded spawn may take longer than the launch's step rounds; with a budget each
-        // spawning wave parks its spawn after that many cycles and a later launch resumes it (the spawn is
-        // needed one whole episode later). Off by default since round 5: with parking on (600 k cycles), 5 of
-        // 149 C3 runs of 400 launches departed from the others in one env (a spawn's last humans), 0 of 208
-        // without; since the candidate-box covers made crowded spawns ~2.3x cheaper, parking is worth only
-        // 1.7 % of C3 steady state (423 vs 430 us). The quad path's spawns are short: never parked.
-        g->spawn_budget = 0;
+        // kd-tree path: a crowded spawn may take longer than the launch's step rounds; each spawning wave parks
+        // its spawn after ~0.6 M cycles and a later launch resumes it (the spawn is needed one whole episode
+        // later). Round 5: spawn-list entries carry the counters of the reset that queued them (a spawn wave
+        // that read them from the state could see a later reset of the same env and queue a key that the next
+        // launch queued again: two writers of one pending slot, one of them resuming from it -- 5 of 149 C3 runs
+        // departed; 0 of 149 with keyed entries). The quad path's spawns are short: never parked.
+        g->spawn_budget = 600000;
     }
     cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
     if (circ_table_init() != hipSuccess) {
@@ -4313,7 +4329,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.E = g->E;
     a.case_size = g->case_size;
     a.ctl = g->work_count; a.plist_base = g->plist; a.rlist_base = g->rlist;
-    a.plist_w = g->plist + (int64_t)kw * (g->E + 64);
+    a.plist_w = g->plist + (int64_t)kw * 4 * (g->E + 64);
     a.pcount_w = g->work_count + 2 + kw;
     a.pcount_zero = g->work_count + 2 + kz;
     a.rcount_zero = g->work_count + 5 + kz;
@@ -4323,7 +4339,7 @@ int cn_step(cn_engine *g, void *stream, const float *actions, float *robot_node,
     a.pend.stats = g->work_count + 8;
     a.pend.launch_id = (uint32_t)(g->nstep % 0x7ffffffeu) + 1u;   // nonzero, differs from the neighbours'
     const int blocks = (g->E + g->plan.EPB - 1) / g->plan.EPB;
-    a.pend.P = g->pend; a.pend.list = g->plist + (int64_t)kr * (g->E + 64); a.pend.count = g->work_count + 2 + kr;
+    a.pend.P = g->pend; a.pend.list = g->plist + (int64_t)kr * 4 * (g->E + 64); a.pend.count = g->work_count + 2 + kr;
     a.pend.all = g->pend_all;
     a.pend.step_blocks = blocks; a.pend.pend_blocks = g->pend_blocks; a.pend.counter_offset = g->counter_offset;
     a.pend.first = g->plan.kd ? 1 : 0;

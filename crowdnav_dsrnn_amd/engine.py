@@ -190,8 +190,8 @@ class CrowdNavEngine:
 
     def set_spawn_budget(self, cycles):
         """Test hook (cn_debug_set_spawn_budget): clock cycles a kd-tree-path spawning wave works per launch
-        before it parks its spawn (default 0 = never; parking showed a rare run-to-run departure, DESIGN.md
-        round 5, and is kept for the tests that exercise it)."""
+        before it parks its spawn (default 600000; 0 = never). Results do not depend on it (round 5 fixed a rare
+        case where they did: DESIGN.md)."""
         _lib.check(_lib.lib().cn_debug_set_spawn_budget(self._h, int(cycles)))
 
     def spawn_stats(self):

@@ -435,8 +435,7 @@ int cn_social_force_predict(void *stream, int64_t n, int M, const double *self, 
 
 /* Test hooks of the kd-tree path's resumable spawns (the spawn waves that draw upcoming episodes park a
  * crowded spawn between two humans once a wave has worked `cycles` clock cycles in a launch, and a later
- * launch resumes it; default 0 = never park (parking showed a rare run-to-run departure);
- * no effect on the quad path, which never parks).
+ * launch resumes it; default 600000, 0 = never park; no effect on the quad path, which never parks).
  * cn_debug_spawn_stats: cumulative counts since cn_create [5] = spawns parked before they started, parked
  * mid-way, resumed, completed by a resume (kd-tree path), and auto-resets whose spawn the step kernel drew
  * inline because no pending spawn was ready (every path; synchronises the device). Results do not depend on the budget:

@@ -303,9 +303,8 @@ def _c3_engine(E):
 def test_c3_first_launches_find_their_spawns_and_runs_repeat():
     """The kd-tree path after cn_reset (C3 shape, 1024 envs x 25 humans, 60 launches): the reset kernel draws
     every env's next two spawns, so no reset of the first launches draws a crowded spawn inline; and runs from
-    the same reset and actions end in the same state bit for bit -- at the default (no spawn parking) and with
-    the spawn waves parking after every human (20 k cycles), which round 5 found to depart in rare cases at
-    C3's full size but not at this size and length."""
+    the same reset and actions end in the same state bit for bit, at the default spawn budget (spawns parked
+    and resumed at run-dependent points) and with the spawn waves parking after every human (20 k cycles)."""
     E, T = 1024, 60
     g = torch.Generator(device="cuda:0").manual_seed(11)
     acts = (torch.randn((T, E, 2), generator=g, device="cuda:0") * 0.5).contiguous()

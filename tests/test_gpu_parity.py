@@ -263,9 +263,8 @@ def test_gpu_full_size_c3_free_running(gpu, oracle):
     holonomic: the kd-tree path, the bench's --workload c3) for 400 free-running steps: the first 40 steps
     identical to the oracle, then finite outputs, done exactly where the event is terminal, Monitor lengths
     within the time limit, each env's reset count = 1 + its episodes ended, episode counts / mean return
-    within 2 % of the oracle's over the 400 steps, and the spawn counters show spawns parked and resumed under
-    round 4's 600 k-cycle budget (the crowded spawns of this workload outlast it; parking is off by default
-    since round 5)."""
+    within 2 % of the oracle's over the 400 steps, and the spawn counters show spawns parked and resumed at
+    the default 600 k-cycle budget (the crowded spawns of this workload outlast it)."""
     E = 4096
     cfg = _cfg(25, "holonomic", "square_crossing", E=E, fov=1.0)
     oracle.lib().cnref_set_threads(min(16, os.cpu_count() or 1))
