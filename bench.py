@@ -782,14 +782,24 @@ def run_side_windows(torch, dist, device, rank, world, rng, line, launch="seq"):
     import threading
 
     t_start = time.perf_counter()
+    # side results enter `line` only under this lock, so the watchdog serialises a consistent snapshot
+    lock = threading.Lock()
 
     def bail():
+        # a side window that hangs (or a rank stuck in a collective after another rank's exception) ends the
+        # process with a non-zero status: the main measurement is printed first, but the run did not finish
         if rank == 0 and line is not None:
-            line["side_timeout_s"] = SIDE_DEADLINE_S
-            print(json.dumps(line), flush=True)
+            got = lock.acquire(timeout=5.0)
+            try:
+                snap = dict(line)
+            finally:
+                if got:
+                    lock.release()
+            snap["side_timeout_s"] = SIDE_DEADLINE_S
+            print(json.dumps(snap), flush=True)
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(3)
 
     timer = threading.Timer(SIDE_DEADLINE_S, bail)
     timer.daemon = True
@@ -818,11 +828,13 @@ def run_side_windows(torch, dist, device, rank, world, rng, line, launch="seq"):
             torch.cuda.empty_cache()
             if rank == 0:
                 obj["wall_s"] = round(time.perf_counter() - t0, 2)
-                line["side_" + wl] = obj
+                with lock:
+                    line["side_" + wl] = obj
     finally:
         timer.cancel()
     if rank == 0:
-        line["side_wall_s"] = round(time.perf_counter() - t_start, 2)
+        with lock:
+            line["side_wall_s"] = round(time.perf_counter() - t_start, 2)
 
 
 def roofline_obj(achieved, bpl, pmc):

@@ -136,7 +136,7 @@ def lib():
         L.cn_gru_fwd_step_group.restype = i32
         L.cn_gru_fwd_seq.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqFwd)]
         L.cn_gru_fwd_seq.restype = i32
-        L.cn_gru_bwd_seq.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqBwd), vp]
+        L.cn_gru_bwd_seq.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(GruSeqBwd), vp, i64]
         L.cn_gru_bwd_seq.restype = i32
         L.cn_set_graph_mode.argtypes = [vp, vp, ctypes.c_int]
         L.cn_graph_node_counts.argtypes = [vp, ctypes.POINTER(i64), ctypes.c_int, ctypes.POINTER(i64)]

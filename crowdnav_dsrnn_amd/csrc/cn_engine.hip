@@ -2226,16 +2226,15 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         bool started = false;
         if (it < nnew) {
             const bool ahead2 = (GRID ? pl.all != PEND_BOTH : !pl.all) || it >= (uint32_t)E;
-            if (pl.all) {   // cn_set_state: the state's counters (no step launch is rewriting them)
-                e = (int64_t)(it % (uint32_t)E);
-                cc = S.case_counter[e];
-                rc = S.reset_count[e];
-            } else {        // the counters the previous launch's reset wrote (carried by the list entry)
-                const uint32_t *q = pl.list + 4 * it;
-                e = (int64_t)q[0];
-                rc = (int32_t)q[1];
-                cc = (int64_t)((uint64_t)q[2] | ((uint64_t)q[3] << 32));
-            }
+            // the key's counters come from a list entry, never from the state: the step workgroups of this
+            // same launch reset terminal envs and rewrite reset_count / case_counter while the spawn waves run.
+            // PEND_BOTH: cn_keysnap_kernel's snapshot of every env's counters, written (stream-ordered) by
+            // cn_set_state / cn_reset before this launch (entry e for items e and e + E); otherwise the
+            // counters the previous launch's reset wrote (round 5: read back by the resetting wave)
+            const uint32_t *q = pl.list + 4 * (pl.all ? it % (uint32_t)E : it);
+            e = (int64_t)q[0];
+            rc = (int32_t)q[1];
+            cc = (int64_t)((uint64_t)q[2] | ((uint64_t)q[3] << 32));
             if (ahead2) { cc = (cc + c.nenv) % pl.case_size; rc += 1; }   // write_reset's counter update
         } else {
             const uint32_t *q = pl.rlist + 4 * (it - nnew);
@@ -2243,7 +2242,11 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
             started = (q[0] >> 31) == 0u;
             rc = (int32_t)q[1];
             cc = (int64_t)((uint64_t)q[2] | ((uint64_t)q[3] << 32));
-            if (rc < S.reset_count[e]) continue;   // its reset has come and gone (drawn inline)
+            // its reset has come and gone (drawn inline). reset_count may be advanced by a reset of this same
+            // launch while it is read; either value is safe: such a reset draws inline (the parked entry is not
+            // complete), so the item only turns stale, and the next writer of its slot (key rc + 2, queued by
+            // that reset) belongs to the next launch, stream-ordered after this item's stores
+            if (rc < S.reset_count[e]) continue;
         }
         if (deadline && worked && (long long)clock64() > deadline) {   // out of budget: park the item unstarted / as is
             if (lane == 0) {
@@ -3373,6 +3376,8 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             }
         }
         }
+        // back to normal priority for the epilogue (graph mode's finish barrier, stamps)
+        if ((KD || CN_RNG_PRIO_ALL) && w < nw) __builtin_amdgcn_s_setprio(0);
     }
 #ifdef CN_STAMPS
     __syncthreads();
@@ -3922,6 +3927,34 @@ static int ctl_set(uint32_t *w, uint32_t v, hipStream_t st)
     return e == hipSuccess ? CN_OK : set_err(CN_EHIP, hipGetErrorString(e));
 }
 
+// Key snapshot for a PEND_BOTH launch (after cn_set_state, and the quad path's cn_reset): every env's
+// {e, reset_count, case_counter lo, hi} into the spawn list the next step launch reads (kr = (t + 2) % 3 for
+// launch t: the host's sequence number, or graph mode's device word). That launch's spawn waves key both of an
+// env's pending spawns from this entry, not from the state its own step workgroups rewrite when a terminal env
+// resets inline (crowd_sim_dict.py:147-164: the seed of the k-th reset is offset + case_counter + thisSeed).
+__global__ void cn_keysnap_kernel(const int32_t *__restrict__ reset_count, const int64_t *__restrict__ case_counter,
+                                  uint32_t *plist_base, const uint32_t *ctl, int host_kr, int E)
+{
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= E) return;
+    const int64_t kr = host_kr >= 0 ? host_kr : (int64_t)((ctl[CN_CTL_NSTEP] + 2u) % 3u);
+    uint32_t *q = plist_base + kr * 4 * ((int64_t)E + 64) + 4 * (int64_t)e;
+    const uint64_t cc = (uint64_t)case_counter[e];
+    const uint4 v = make_uint4((uint32_t)e, (uint32_t)reset_count[e], (uint32_t)cc, (uint32_t)(cc >> 32));
+    *(uint4 *)q = v;
+}
+
+// the snapshot for the engine's next step launch (g->nstep: the host sequence; graph mode reads the device's)
+static int keysnap(const cn_engine *g, hipStream_t st)
+{
+    const int host_kr = g->devseq ? -1 : (int)((g->nstep + 2) % 3);
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(cn_keysnap_kernel, dim3((g->E + 255) / 256), dim3(256), 0, st, g->s.reset_count, g->s.case_counter,
+                       g->plist, (const uint32_t *)g->work_count, host_kr, (int)g->E);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? CN_OK : set_err(CN_EHIP, hipGetErrorString(e));
+}
+
 extern "C" {
 
 int cn_graph_node_counts(void *graph, int64_t *counts, int n, int64_t *total)
@@ -4098,6 +4131,8 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         for (const void *k : ks) (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g->a_lds);
     }
     g->rng_grid = g->E < 2048 ? g->E : 2048;
+    // the first launch draws every env's spawns (PEND_BOTH) from the key snapshot of the zeroed state
+    if (keysnap(g, nullptr) != CN_OK) { cn_destroy(g); return CN_EHIP; }
     HIPCHK(hipDeviceSynchronize());
     *out = g;
     return CN_OK;
@@ -4291,6 +4326,10 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     // draws them (none) and ignores the earlier launches' lists (host flag; graph mode: the device flag,
     // stream-ordered)
     g->pend_all = a.draw_next ? PEND_FRESH : PEND_BOTH;
+    if (!a.draw_next) {   // PEND_BOTH keys its items from a snapshot of the counters the reset kernel wrote
+        const int rk = keysnap(g, st);
+        if (rk) return rk;
+    }
     if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, (uint32_t)g->pend_all, st);
     return CN_OK;
 }
@@ -4453,8 +4492,11 @@ int cn_set_state(cn_engine *g, void *stream, const void *src, int src_on_host)
     } else {
         HIPCHK(hipMemcpyAsync(g->state, src, g->state_bytes, hipMemcpyDeviceToDevice, st));
     }
-    // pending spawns are keyed by (case_counter, reset_count); redraw them for the new state
+    // pending spawns are keyed by (case_counter, reset_count); redraw them for the new state, keyed from a
+    // snapshot of its counters (the next launch's own resets rewrite the state's while its spawn waves run)
     g->pend_all = PEND_BOTH;
+    const int rk = keysnap(g, st);
+    if (rk) return rk;
     if (g->devseq) return ctl_set(g->work_count + CN_CTL_ALL, PEND_BOTH, st);
     return CN_OK;
 }

@@ -1233,7 +1233,7 @@ int64_t cn_gru_bwd_seq_work_elems(int T, int H, int nseg, const cn_gru_seq_bwd *
     return n;
 }
 
-int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs, float *work)
+int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs, float *work, int64_t work_elems)
 {
     if (T <= 0 || H <= 0 || H % GF_BU || nseg < 1 || nseg > 2 || !segs)
         return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: T > 0, H % 32 == 0 and 1 <= nseg <= 2 required");
@@ -1246,6 +1246,10 @@ int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *s
         if (!aligned16({q.w_hh_t, q.dout, q.save, q.hm, q.acc, q.g}))
             return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: w_hh_t, dout, save, hm, acc and g must be 16-byte aligned");
     }
+    // the row tiling (and with it the workspace) follows the CU count of the CURRENT device: a workspace sized on
+    // another device may be too small for this one's choice
+    if (work_elems < cn_gru_bwd_seq_work_elems(T, H, nseg, segs))
+        return cn_set_error(CN_EINVAL, "cn_gru_bwd_seq: workspace smaller than cn_gru_bwd_seq_work_elems on this device");
     const int ut = H / GF_BU;
     const int64_t bm = row_tile(segs[0].B + (nseg > 1 ? segs[1].B : 0), H);
     const int64_t rt0 = bwd_part_rows(segs[0].B, bm), rt1 = nseg > 1 ? bwd_part_rows(segs[1].B, bm) : 0;

@@ -101,6 +101,9 @@ class RolloutTrainer:
                     warnings.warn("rollout HIP-graph capture failed (%s); running eagerly" % e)
                     self.graphs = False
                     g = None
+                    # eager cn_step launches take the host-sequenced kernels again (the capture recorded
+                    # nothing that ran, so the device sequence words still equal the host's)
+                    self.envs.engine.set_graph_mode(False)
                 r.step = step0
                 if g is not None:
                     # no memset nodes: this ROCm runtime can replay a memset node with stale bytes instead of its
@@ -112,6 +115,7 @@ class RolloutTrainer:
                                       % (self.graph_audit["memset"], self.graph_audit))
                         self.graphs = False
                         g = None
+                        self.envs.engine.set_graph_mode(False)
                     else:
                         g.instantiate()
                 self._graph = g

@@ -371,9 +371,10 @@ class _MaskedGRUSeq(torch.autograd.Function):
                                    save.data_ptr(), hm.data_ptr(), acc.data_ptr(), g.data_ptr(), db[0].data_ptr(),
                                    db[1].data_ptr())
             keep.append((acc, dout, g, db, wt))
-        work = torch.empty((L.cn_gru_bwd_seq_work_elems(T, H, nseg, bs),), dtype=torch.float32, device=dev)
-        with torch.cuda.device(dev):
-            _lib.check(L.cn_gru_bwd_seq(st, T, H, nseg, bs, work.data_ptr()))
+        with torch.cuda.device(dev):   # the workspace size follows the device the backward runs on
+            nw = L.cn_gru_bwd_seq_work_elems(T, H, nseg, bs)
+            work = torch.empty((nw,), dtype=torch.float32, device=dev)
+            _lib.check(L.cn_gru_bwd_seq(st, T, H, nseg, bs, work.data_ptr(), nw))
             res = [None]
             for i in range(nseg):
                 x2, m, w_ih, w_hh, hm, save = sv[6 * i:6 * i + 6]

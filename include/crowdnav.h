@@ -379,8 +379,9 @@ int64_t cn_gru_bwd_seq_work_elems(int T, int H, int nseg, const cn_gru_seq_bwd *
  * acc_t = a_t + dgh_t W_hh of one step on the f32 matrix cores with the gate gradients of the step before in
  * its epilogue (cn_gru_bwd_step_gates' arithmetic; launches with fewer 128-row tiles than CUs split K over
  * the workgroup's waves on 32-row tiles), then the bias reduction; replaces the per-step
- * cn_gru_bwd_step_gates + GEMM pair. */
-int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs, float *work);
+ * cn_gru_bwd_step_gates + GEMM pair. work_elems = the floats at work; fails (CN_EINVAL) when it is below
+ * cn_gru_bwd_seq_work_elems on the current device. */
+int cn_gru_bwd_seq(void *stream, int T, int H, int nseg, const cn_gru_seq_bwd *segs, float *work, int64_t work_elems);
 
 /* The ConvGRU observation row of every env, obs [E][7 + beams] float32:
  *   [clip(robot (px, py, radius, gx, gy, v_pref, theta) / max_range, 0, 1), scan].

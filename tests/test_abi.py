@@ -58,9 +58,16 @@ def test_gru_seq_rejects_bad_arguments_without_launching(L):
     assert L.cn_gru_bwd_seq_work_elems(3, 256, 2, bsegs) == (3 * 176 + 64) * 1024
     bsegs[0].B = 2048   # 16 x 4 tiles of 128 rows < 256 CUs: split-K on 32-row tiles (64 per step)
     assert L.cn_gru_bwd_seq_work_elems(2, 128, 1, bsegs) == (2 * 64 + 64) * 512
-    assert L.cn_gru_bwd_seq(None, 0, 256, 1, bsegs, None) != 0     # T = 0
-    assert L.cn_gru_bwd_seq(None, 4, 256, 1, bsegs, None) != 0
+    assert L.cn_gru_bwd_seq(None, 0, 256, 1, bsegs, None, 0) != 0     # T = 0
+    assert L.cn_gru_bwd_seq(None, 4, 256, 1, bsegs, None, 0) != 0
     assert b"cn_gru_bwd_seq" in L.cn_last_error()
+    # a workspace below the size for the current device is rejected before any launch (the split-K
+    # choice follows the device's CU count; dummy 16-byte aligned operands are never dereferenced)
+    one = (_lib.GruSeqBwd * 1)()
+    one[0] = _lib.GruSeqBwd(2048, 16, 32, 48, 64, 80, 96, 112, 128, 144)
+    need = L.cn_gru_bwd_seq_work_elems(2, 128, 1, one)
+    assert L.cn_gru_bwd_seq(None, 2, 128, 1, one, 4096, need - 1) != 0
+    assert b"workspace smaller" in L.cn_last_error()
     # masked-state ring: nh >= 2 when T > 1 (a step reads hm[t % nh] while other workgroups write
     # hm[(t + 1) % nh]); nh == T with save (the backward reads every step's hm). Rejected before any launch
     # (non-null dummy addresses, 16-byte aligned, are never dereferenced)

@@ -247,15 +247,74 @@ def test_gpu_forced_spawn_parking_matches_oracle(gpu, oracle):
         g.eng.set_spawn_budget(1)
         ref.reset()
         g.reset()
-        _free_run_exact(ref, g, cfg, 100, "holonomic", 17)
+        _free_run_exact(ref, g, cfg, 200, "holonomic", 17)
         rs, gs = ref.get_state(), g.get_state()
         d = {"post_" + n: np.asarray(getattr(rs, n)) for n, _, _ in abi.STATE_FIELDS if n != "mt"}
         d["post_mt_crc"] = H.mt_crc(rs)
         errs = H.compare_state(gs, d, "post_", tol=1e-5)
         assert not errs, errs
         st = g.eng.spawn_stats()
-        # (cn_reset draws every env's next two spawns itself, so the spawn waves' work starts at the third)
-        assert st["parked_midway"] > 1000 and st["resumed"] > 1000 and st["completed_on_resume"] > 25, (rngmode, st)
+        # (cn_reset draws every env's next two spawns itself, so the spawn waves' work starts at the third: 200
+        # launches instead of round 4's 100 keep the resume path's coverage floor at 50 completions)
+        assert st["parked_midway"] > 1000 and st["resumed"] > 1000 and st["completed_on_resume"] > 50, (rngmode, st)
+
+
+@pytest.mark.parametrize("shape,budget,start,tl", [
+    ("c3", None, "reset", 1), ("c3", None, "set_state", 1), ("c3", None, "set_state", 2),
+    ("c3", 1, "set_state", 1), ("c3", 1, "set_state", 2),
+    ("c2", None, "reset", 1), ("c2", None, "set_state", 1), ("c2", None, "set_state", 2),
+])
+def test_gpu_every_env_resets_every_launch(gpu, oracle, shape, budget, start, tl):
+    """Spawn-key races. time_limit = 1 makes every env time out at its first step
+    (crowd_sim.py:1032-1035: global_time >= time_limit - 1), so every env auto-resets in every launch
+    (shmem_vec_env.py:164-168) and draws its next episode from the seed schedule (crowd_sim_dict.py:147-164);
+    time_limit = 2 ends episodes after at most 4 steps, so a pending spawn waits a few launches before a reset
+    consumes it. Both races key a spawn item from counters that a reset of the SAME launch rewrites: round 5's
+    list path (an env resetting twice before its spawn is keyed) and the draw-both launch after cn_set_state /
+    the quad path's cn_reset (PEND_BOTH: the step workgroups' inline resets advance reset_count / case_counter
+    while the spawn waves key both pending slots; now keyed from cn_keysnap_kernel's snapshot). The state is
+    re-loaded every 8 launches (from the oracle's), so a run holds eight draw-both launches. kd-tree path (C3
+    shape; E = 1000, so an env's two items of a draw-both launch go to different spawning waves) at the default
+    spawn budget and at a 1-cycle budget (E = 192 < 256 spawning waves, so parked spawns are resumed), quad path
+    (C2 shape, 4096 envs); 64 launches each: done / event exact and rewards 1e-5 every launch, the whole state
+    and every MT19937 stream at the end."""
+    E = 4096 if shape == "c2" else (192 if budget == 1 else 1000)
+    if shape == "c3":
+        cfg = _cfg(25, "holonomic", "square_crossing", E=E, fov=1.0, env__time_limit=tl)
+    else:
+        cfg = _cfg(10, "unicycle", E=E, env__time_limit=tl)
+    oracle.lib().cnref_set_threads(min(16, os.cpu_count() or 1))
+    ref, g = oracle.RefEngine(cfg), gpu(cfg)
+    if budget is not None:
+        g.eng.set_spawn_budget(budget)
+    ref.reset()
+    if start == "reset":
+        g.reset()
+    kind = "holonomic" if shape == "c3" else "unicycle"
+    rng = np.random.RandomState(23)
+    resets = 0
+    for t in range(64):
+        if start == "set_state" and t % 8 == 0:
+            g.set_state(ref.get_state())
+        a = (rng.uniform(-0.1, 0.1, (E, 2)) if kind == "unicycle" else rng.normal(0, 0.5, (E, 2))).astype(np.float32)
+        r1, r2 = ref.step(a), g.step(a)
+        if tl == 1:
+            assert r1[2].all(), "time_limit = 1: every env ends its episode at every step (t=%d)" % t
+        resets += int(r1[2].sum())
+        np.testing.assert_array_equal(r2[2], r1[2], err_msg="done t=%d" % t)
+        np.testing.assert_array_equal(r2[3], r1[3], err_msg="event t=%d" % t)
+        np.testing.assert_allclose(r2[1], r1[1], atol=1e-5, rtol=0, err_msg="reward t=%d" % t)
+    assert resets >= 64 * E // 6, resets   # episodes of at most 5 steps
+    rs, gs = ref.get_state(), g.get_state()
+    d = {"post_" + n: np.asarray(getattr(rs, n)) for n, _, _ in abi.STATE_FIELDS if n != "mt"}
+    d["post_mt_crc"] = H.mt_crc(rs)
+    errs = H.compare_state(gs, d, "post_", tol=1e-5)
+    assert not errs, errs[:20]
+    if shape == "c3" and budget == 1:
+        st = g.eng.spawn_stats()
+        assert st["parked_midway"] > 0, st
+        if tl == 2:   # at time_limit = 1 every wave's first item is a new spawn, so parked ones are never resumed
+            assert st["resumed"] > 0, st
 
 
 def test_gpu_full_size_c3_free_running(gpu, oracle):

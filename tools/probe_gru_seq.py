@@ -58,7 +58,7 @@ def case(name, Bs, H, T=16, reps=3, F=0):
         return e0.elapsed_time(e1) * 1e3 / reps / launches
 
     tf = timed(lambda: _lib.check(L.cn_gru_fwd_seq(st, T, H, len(Bs), fs)), T)
-    tb = timed(lambda: _lib.check(L.cn_gru_bwd_seq(st, T, H, len(Bs), bs, work.data_ptr())), T + 1)
+    tb = timed(lambda: _lib.check(L.cn_gru_bwd_seq(st, T, H, len(Bs), bs, work.data_ptr(), work.numel())), T + 1)
     rows = sum(Bs)
     fl = 2.0 * rows * H * 3 * H
     flf = 2.0 * rows * (H + F) * 3 * H
