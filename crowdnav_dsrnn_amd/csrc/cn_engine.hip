@@ -388,28 +388,38 @@ __device__ inline bool inside_world(double px, double py, double r, double half)
     return !(right || left || top || bottom);
 }
 
-__device__ inline void norm_zone(double px, double py, double vx, double vy, double r, bool f32, int lhs, int left,
-                                 double *cx, double *cy)
+// The robot's heading frame of its norm zones (both zones share it): offset point and rotation by dth
+struct ZoneFrame {
+    double dth, xos, yos, c, s;
+};
+
+__device__ __forceinline__ ZoneFrame zone_frame(double px, double py, double vx, double vy, double r, bool f32)
 {
-    const double w = 2 * r * 1.5, len = 1.5 * 1.2;
-    double dth, xos, yos;
+    ZoneFrame f;
     if (f32) {
         const float h = atan2f((float)vy, (float)vx);
-        dth = (double)(h - (float)(CN_PI / 2));
-        xos = px + (double)((float)r * np_cosf(h));
-        yos = py + (double)((float)r * np_sinf(h));
+        f.dth = (double)(h - (float)(CN_PI / 2));
+        f.xos = px + (double)((float)r * np_cosf(h));
+        f.yos = py + (double)((float)r * np_sinf(h));
     } else {
         const double heading = atan2(vy, vx);
-        dth = heading - CN_PI / 2;
-        xos = px + r * cos(heading);
-        yos = py + r * sin(heading);
+        f.dth = heading - CN_PI / 2;
+        f.xos = px + r * cos(heading);
+        f.yos = py + r * sin(heading);
     }
+    f.c = cos(f.dth); f.s = sin(f.dth);
+    if (fabs(f.c) < 2.5e-16) f.c = 0.0;
+    if (fabs(f.s) < 2.5e-16) f.s = 0.0;
+    return f;
+}
+
+__device__ inline void norm_zone(const ZoneFrame &f, double r, int lhs, int left, double *cx, double *cy)
+{
+    const double w = 2 * r * 1.5, len = 1.5 * 1.2;
+    const double xos = f.xos, yos = f.yos, c = f.c, s = f.s;
     double tx, ty;
     if (lhs) { if (left) { tx = -w / 2; ty = len / 2 + 0.6; } else { tx = w / 2; ty = len / 2; } }
     else { if (left) { tx = -w / 2; ty = len / 2; } else { tx = w / 2; ty = len / 2 + 0.6; } }
-    double c = cos(dth), s = sin(dth);
-    if (fabs(c) < 2.5e-16) c = 0.0;
-    if (fabs(s) < 2.5e-16) s = 0.0;
     const double bx[4] = {w / 2, w / 2, -w / 2, -w / 2};
     const double by[4] = {-len / 2, len / 2, len / 2, -len / 2};
 #pragma unroll
@@ -454,12 +464,36 @@ __device__ __forceinline__ void gon_extent(double px, double py, double r, doubl
     }
 }
 
+// One 64-gon edge axis of disc_quad_sat's second loop (edge k -> k + 1, extents over the +-2 vertex windows
+// of gon_extent): true if it separates the 64-gon from the quad. Same vertices, same operations as the loop.
+__device__ __forceinline__ bool gon_axis_separates(double px, double py, double r, const double *qx, const double *qy, int k)
+{
+    auto vx = [&](int idx) { idx &= 63; return idx == 0 ? px + r : px + r * c_circ_cos[idx]; };
+    auto vy = [&](int idx) { idx &= 63; return idx == 0 ? py : py + r * c_circ_sin[idx]; };
+    const double ex = vx(k + 1) - vx(k), ey = vy(k + 1) - vy(k);
+    if (ex == 0.0 && ey == 0.0) return false;
+    const double nx = -ey, ny = ex;
+    double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
+#pragma unroll
+    for (int d = 0; d < 5; ++d) {
+        const double t = vx(k - 2 + d) * nx + vy(k - 2 + d) * ny;
+        const double u = vx(k + 30 + d) * nx + vy(k + 30 + d) * ny;
+        amax = t > amax ? t : amax;
+        amin = u < amin ? u : amin;
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
+    return amax < bmin || bmax < amin;
+}
+
 // Separating-axis test over the edge normals of the quad and of the 64-gon (the predicate the oracle,
-// oracle/cpu_ref.c:disc_quad_intersect, evaluates with all 64 vertices per axis): identical boolean.
+// oracle/cpu_ref.c:disc_quad_intersect, evaluates with all 64 vertices per axis): identical boolean. Only the
+// fallback for degenerate quads / radii (and the test hook's mode 1), so written for few registers: loops
+// not unrolled.
 __device__ __forceinline__ bool disc_quad_sat(double px, double py, double r, const double *qx, const double *qy)
 {
     const double step = CN_PI / 32;
-#pragma unroll
+#pragma unroll 1
     for (int k = 0; k < 4; ++k) {   // quad edges: the 64-gon's extreme vertex from the axis angle
         const int k1 = (k + 1) & 3;
         const double ex = qx[k1] - qx[k], ey = qy[k1] - qy[k];
@@ -472,48 +506,61 @@ __device__ __forceinline__ bool disc_quad_sat(double px, double py, double r, co
         for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
         if (amax < bmin || bmax < amin) return false;
     }
-    // 64-gon edge k -> k+1: its normal (-ey, ex) points at angle -(k + 1/2) pi/32. The loop index is
-    // wave-uniform, so the unit-circle entries of the +-2 windows (vertices k-2..k+2 and k+30..k+34, as in
-    // gon_extent) slide along in registers and the two new entries are loaded one iteration ahead: the
-    // loop was bound by the latency of its table loads. Same vertices, same operations.
-    double wc[5], ws[5], oc[5], os[5];
+#pragma unroll 1
+    for (int k = 0; k < 64; ++k)   // 64-gon edge k -> k+1 (its normal points at -(k + 1/2) pi/32)
+        if (gon_axis_separates(px, py, r, qx, qy, k)) return false;
+    return true;
+}
+
+// disc_quad_sat for a centre P OUTSIDE the quad within the boundary band (r cos(pi/64) - eps <= d <= r + eps,
+// d = |c - P|, c the quad's closest point, (cx, cy) = c - P): the same boolean from the 4 quad axes and only
+// the 64-gon edge axes whose direction lies within 3 steps of c - P or of P - c. Why no other axis can
+// separate: an axis of unit direction u separates (amax < bmin) only if min_q (q - P).u exceeds the 64-gon's
+// support (v - P).u, which is at least the apothem r cos(pi/64) for every u; but min_q (q - P).u <=
+// (c - P).u = d cos(angle(u, c - P)) <= (r + eps) cos(angle). Edge k's normal points at -(k + 1/2) pi/32;
+// ks, the nearest such edge to c - P, is within pi/64 (+ rounding of atan2 / rint) of it, so an edge 4 or
+// more steps away is >= 3.5 pi/32 off: (r + eps) cos(3.5 pi/32) = 0.941 (r + eps) < 0.9988 r -- a margin of
+// ~0.057 r against eps = 1e-9 and the ~1e-15 r rounding of the projections (r > 1e-6 here). The other
+// condition (bmax < amin) is separation along -u: the window around ks + 32. SURVEY §9-7; the 100 k predicate
+// cases of tests/test_norm_zone.py (the zones' corner-on-circle geometry included) check it against the
+// oracle's all-axes test.
+// kq >= 0: the quad is a norm zone (a rectangle rotated by dth, norm_zone), whose edge k's normal points at
+// dth + pi + k pi/2, so the 64-gon's extreme vertex for it is (kq - 16 k) & 63 with kq = rint(-dth / step) - 32
+// -- the vertex nearest the normal up to one step where the rounded edge vector's atan2 would round the other
+// way, which gon_extent's +-2 window absorbs (its extremes are those of all 64 vertices for any kmax within one
+// step of the nearest vertex): the same amin / amax, without four f64 atan2. kq < 0: atan2 per edge.
+__device__ __forceinline__ bool disc_quad_sat_band(double px, double py, double r, const double *qx, const double *qy,
+                                                   double cx, double cy, int kq)
+{
+    const double step = CN_PI / 32;
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {   // quad edges, as in disc_quad_sat
+        const int k1 = (k + 1) & 3;
+        const double ex = qx[k1] - qx[k], ey = qy[k1] - qy[k];
+        if (ex == 0.0 && ey == 0.0) continue;
+        const double nx = -ey, ny = ex;
+        const int kmax = kq >= 0 ? (kq - 16 * k) & 63 : ((int)rint(-atan2(ny, nx) / step) % 64 + 64) % 64;
+        double amin, amax, bmin = INFINITY, bmax = -INFINITY;
+        gon_extent(px, py, r, nx, ny, kmax, amin, amax);
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
-        wc[i] = c_circ_cos[(i - 2) & 63]; ws[i] = c_circ_sin[(i - 2) & 63];
-        oc[i] = c_circ_cos[(30 + i) & 63]; os[i] = c_circ_sin[(30 + i) & 63];
+        for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
+        if (amax < bmin || bmax < amin) return false;
     }
-    auto vx = [&](int idx, double cs) { return (idx & 63) == 0 ? px + r : px + r * cs; };
-    auto vy = [&](int idx, double sn) { return (idx & 63) == 0 ? py : py + r * sn; };
-    for (int k = 0; k < 64; ++k) {
-        const double nc = c_circ_cos[(k + 3) & 63], ns = c_circ_sin[(k + 3) & 63];
-        const double nco = c_circ_cos[(k + 35) & 63], nso = c_circ_sin[(k + 35) & 63];
-        const double ex = vx(k + 1, wc[3]) - vx(k, wc[2]), ey = vy(k + 1, ws[3]) - vy(k, ws[2]);
-        if (!(ex == 0.0 && ey == 0.0)) {
-            const double nx = -ey, ny = ex;
-            double amin = INFINITY, amax = -INFINITY, bmin = INFINITY, bmax = -INFINITY;
-#pragma unroll
-            for (int d = 0; d < 5; ++d) {
-                const double t = vx(k - 2 + d, wc[d]) * nx + vy(k - 2 + d, ws[d]) * ny;
-                const double u = vx(k + 30 + d, oc[d]) * nx + vy(k + 30 + d, os[d]) * ny;
-                amax = t > amax ? t : amax;
-                amin = u < amin ? u : amin;
-            }
-#pragma unroll
-            for (int v = 0; v < 4; ++v) { const double t = qx[v] * nx + qy[v] * ny; bmin = t < bmin ? t : bmin; bmax = t > bmax ? t : bmax; }
-            if (amax < bmin || bmax < amin) return false;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { wc[i] = wc[i + 1]; ws[i] = ws[i + 1]; oc[i] = oc[i + 1]; os[i] = os[i + 1]; }
-        wc[4] = nc; ws[4] = ns; oc[4] = nco; os[4] = nso;
+    const int ks = (int)rint(-atan2(cy, cx) / step - 0.5);
+#pragma unroll 1
+    for (int j = -3; j <= 3; ++j) {
+        if (gon_axis_separates(px, py, r, qx, qy, (ks + j) & 63)) return false;
+        if (gon_axis_separates(px, py, r, qx, qy, (ks + 32 + j) & 63)) return false;
     }
     return true;
 }
 
 __device__ __forceinline__ int disc_quad_classify(double px, double py, double r, const double *qx, const double *qy,
-                                                  double sgn, double eps)
+                                                  double sgn, double eps, double &cx, double &cy)
 {
     bool inside = true;
     double d2 = INFINITY;   // squared distance from P to the quad's boundary segments
+    cx = 0.0; cy = 0.0;     // closest boundary point - P
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int k1 = (k + 1) & 3;
@@ -525,7 +572,7 @@ __device__ __forceinline__ int disc_quad_classify(double px, double py, double r
         t = t < 0 ? 0 : (t > 1 ? 1 : t);
         const double dx = wx - t * ex, dy = wy - t * ey;
         const double dd = dx * dx + dy * dy;
-        d2 = dd < d2 ? dd : d2;
+        if (dd < d2) { d2 = dd; cx = -dx; cy = -dy; }
     }
     if (inside) return 1;
     const double d = sqrt(d2);
@@ -538,30 +585,66 @@ __device__ __forceinline__ int disc_quad_classify(double px, double py, double r
 // Away from the boundary the answer is geometric: the 64-gon lies between the discs of radius
 // r cos(pi/64) and r about P, so a centre distance to the (convex) quad below r cos(pi/64) - eps means
 // intersecting and above r + eps disjoint (eps = 1e-9 >> rounding of the inputs); only the thin band in
-// between runs the separating-axis test.
-__device__ __forceinline__ bool disc_quad_intersect(double px, double py, double r, const double *qx, const double *qy)
+// between runs the separating-axis test (disc_quad_sat_band's axes). Returns 1 / 0, or -1 for a degenerate
+// quad or radius, which the full separating-axis test (disc_quad_sat) decides.
+__device__ __forceinline__ int disc_quad_intersect3(double px, double py, double r, const double *qx, const double *qy,
+                                                    int kq = -1)
 {
     const double eps = 1e-9;
     double area2 = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) area2 += qx[k] * qy[(k + 1) & 3] - qx[(k + 1) & 3] * qy[k];
-    int cls = -1;   // 1 / 0 decided by the distance classification, -1: the separating-axis test decides
-    if (fabs(area2) > 1e-12 && r > 1e-6) cls = disc_quad_classify(px, py, r, qx, qy, area2 > 0 ? 1.0 : -1.0, eps);
-    return cls >= 0 ? cls != 0 : disc_quad_sat(px, py, r, qx, qy);
+    if (!(fabs(area2) > 1e-12 && r > 1e-6)) return -1;
+    double cx, cy;
+    // 1 / 0 decided by the distance classification, -1: the centre is in the band, outside the quad
+    const int cls = disc_quad_classify(px, py, r, qx, qy, area2 > 0 ? 1.0 : -1.0, eps, cx, cy);
+    return cls >= 0 ? cls : (int)disc_quad_sat_band(px, py, r, qx, qy, cx, cy, kq);
+}
+
+__device__ __forceinline__ bool disc_quad_intersect(double px, double py, double r, const double *qx, const double *qy)
+{
+    const int v = disc_quad_intersect3(px, py, r, qx, qy);
+    return v >= 0 ? v != 0 : disc_quad_sat(px, py, r, qx, qy);
 }
 
 // crowd_sim.py:918-926,957-960 (norm zones on): both zones are built around the robot and
-// tested against its own disc. Out of line: the 64-gon separating-axis test would otherwise raise the
-// step kernel's register pressure (and scratch) for every workload, norm zones on or off.
-__device__ __noinline__ bool robot_norm_zone_violation(double px, double py, double vx, double vy, double rr, bool f32,
-                                                       int lhs)
+// tested against its own disc. Out of line: the separating-axis tests would otherwise raise the step
+// kernel's register pressure (and scratch) for every workload, norm zones on or off. Returns 1 / 0, or -1
+// when a zone is degenerate (a robot radius <= 1e-6): robot_norm_zone_violation then decides with the full
+// separating-axis test. Two callees, each without calls of its own: a callee's VGPR count (the highest
+// register it touches, callee-saved ones included when it calls further) is charged to every kernel that
+// calls it, beyond the kernel's launch bounds.
+__device__ __noinline__ int robot_norm_zone_fast(double px, double py, double vx, double vy, double rr, bool f32, int lhs)
 {
     double zx[4], zy[4];
+    const ZoneFrame f = zone_frame(px, py, vx, vy, rr, f32);   // the heading's trigonometry once for both zones
+    const int kq = ((int)rint(-f.dth / (CN_PI / 32)) - 32) & 63;
+#pragma unroll 1
     for (int z = 0; z < 2; ++z) {
-        norm_zone(px, py, vx, vy, rr, f32, lhs, z == 0, zx, zy);
-        if (disc_quad_intersect(px, py, rr, zx, zy)) return true;
+        norm_zone(f, rr, lhs, z == 0, zx, zy);
+        const int v = disc_quad_intersect3(px, py, rr, zx, zy, kq);
+        if (v != 0) return v;
+    }
+    return 0;
+}
+
+__device__ __noinline__ bool robot_norm_zone_full(double px, double py, double vx, double vy, double rr, bool f32, int lhs)
+{
+    double zx[4], zy[4];
+    const ZoneFrame f = zone_frame(px, py, vx, vy, rr, f32);
+#pragma unroll 1
+    for (int z = 0; z < 2; ++z) {
+        norm_zone(f, rr, lhs, z == 0, zx, zy);
+        if (disc_quad_sat(px, py, rr, zx, zy)) return true;
     }
     return false;
+}
+
+__device__ __forceinline__ bool robot_norm_zone_violation(double px, double py, double vx, double vy, double rr, bool f32,
+                                                          int lhs)
+{
+    const int v = robot_norm_zone_fast(px, py, vx, vy, rr, f32, lhs);
+    return v >= 0 ? v != 0 : robot_norm_zone_full(px, py, vx, vy, rr, f32, lhs);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3695,8 +3778,12 @@ __global__ void __launch_bounds__(64) cn_disc_quad_kernel(int64_t n, int mode, c
 {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    out[i] = mode ? disc_quad_sat(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i)
-                  : disc_quad_intersect(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i);
+    if (mode == 2)   // the robot's norm-zone penalty predicate: qx[i] = {vx, f32, ...}, qy[i] = {vy, lhs, ...}
+        out[i] = robot_norm_zone_violation(px[i], py[i], qx[4 * i], qy[4 * i], r[i], qx[4 * i + 1] != 0.0,
+                                           (int)qy[4 * i + 1]);
+    else
+        out[i] = mode ? disc_quad_sat(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i)
+                      : disc_quad_intersect(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i);
 }
 
 // cn_debug_copy64: one wave per segment of `seg` doubles

@@ -398,7 +398,10 @@ int cn_lidar_obs(cn_engine *eng, void *stream, const uint8_t *reset_mask, int en
 /* Test hook: the norm-zone predicate of the step kernel, robot 64-gon (GEOS Point.buffer(r)) vs convex quad
  * (crowd_sim.py norm-zone penalty), for n cases on the device: px, py, r [n], qx, qy [n][4],
  * out [n] (1 = intersecting). mode 0: the kernel's function (classification + separating axes), mode 1:
- * the separating-axis test alone. Checked against oracle/cpu_ref.c:disc_quad_intersect in tests/. */
+ * the separating-axis test alone. Checked against oracle/cpu_ref.c:disc_quad_intersect in tests/.
+ * mode 2: the step kernel's whole norm-zone penalty predicate (both zones built around the robot,
+ * crowd_sim.py:918-926): robot at (px, py) of radius r with velocity (qx[i][0], qy[i][0]), float32 heading
+ * if qx[i][1] != 0, zone side preference lhs = qy[i][1]. */
 int cn_debug_disc_quad(void *stream, int64_t n, int mode, const double *px, const double *py, const double *r,
                        const double *qx, const double *qy, int32_t *out);
 

@@ -737,6 +737,21 @@ EXPORT void cnref_disc_quad(int64_t n, const double *px, const double *py, const
     for (int64_t i = 0; i < n; ++i) out[i] = disc_quad_intersect(px[i], py[i], r[i], qx + 4 * i, qy + 4 * i);
 }
 
+/* test hook: the robot's norm-zone penalty predicate (both zones, crowd_sim.py:918-926,957-960) on n cases */
+EXPORT void cnref_norm_zone_violation(int64_t n, const double *px, const double *py, const double *vx, const double *vy,
+                                      const double *r, const int32_t *f32, int32_t lhs, int32_t *out)
+{
+    for (int64_t i = 0; i < n; ++i) {
+        int v = 0;
+        for (int z = 0; z < 2 && !v; ++z) {
+            double qx[4], qy[4];
+            norm_zone(px[i], py[i], vx[i], vy[i], r[i], f32[i], lhs, z == 0, qx, qy);
+            v = disc_quad_intersect(px[i], py[i], r[i], qx, qy);
+        }
+        out[i] = v;
+    }
+}
+
 /* test hook: how far the robot's norm-zone predicate is from its decision boundary. For each of the two
  * zones (norm_zone, crowd_sim.py:918-926) the separating-axis gap between the robot's 64-gon and the zone
  * over all 68 unit edge normals (> 0 separated by that distance, <= 0 overlapping: max over axes of the

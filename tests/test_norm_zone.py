@@ -115,3 +115,52 @@ def test_gpu_predicate_equals_oracle():
     assert 0.2 < want.mean() < 0.8   # both outcomes well represented
     zw = _oracle(*_zone_cases())
     assert 0.05 < zw.mean() < 0.95, zw.mean()   # the corner-on-circle cases split both ways too
+
+
+@pytest.mark.gpu
+def test_gpu_norm_zone_penalty_predicate_equals_oracle():
+    """The step kernel's whole norm-zone predicate (cn_debug_disc_quad mode 2: both zones built around the robot,
+    crowd_sim.py:918-926, the heading's trigonometry shared by the two zones and the quad edges' extreme 64-gon
+    vertices taken from the heading) against the oracle's (oracle/cpu_ref.c:cnref_norm_zone_violation) on 200 k
+    robot states, float32 and float64 headings, both side preferences. The zones' corner lies on the robot's
+    circle by construction, so the heading's last ulp can decide: a disagreement is accepted only
+    where the oracle's separating-axis margin is within what one heading ulp moves a zone corner (1e-6 m f32,
+    1e-12 m f64), as in the teacher-forced C5 test."""
+    import torch
+
+    from crowdnav_dsrnn_amd import _lib
+
+    L = cpu_ref.lib()
+    L.cnref_norm_zone_violation.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 6 + [ctypes.c_int32, ctypes.c_void_p]
+    L.cnref_norm_zone_margin.argtypes = [ctypes.c_double] * 5 + [ctypes.c_int, ctypes.c_int]
+    L.cnref_norm_zone_margin.restype = ctypes.c_double
+    rng = np.random.RandomState(7)
+    n = 100000
+    dev = torch.device("cuda:0")
+    flips = 0
+    for lhs in (0, 1):
+        px, py = rng.uniform(-6, 6, n), rng.uniform(-6, 6, n)
+        sp = rng.uniform(0, 1.2, n)
+        sp[: n // 50] = 0.0                      # standing robots: heading atan2(0, 0)
+        h = rng.uniform(-np.pi, np.pi, n)
+        h[n // 50: n // 10] = np.round(h[n // 50: n // 10] / (np.pi / 32)) * (np.pi / 32)   # on 64-gon axes
+        vx, vy = sp * np.cos(h), sp * np.sin(h)
+        r = rng.uniform(0.2, 0.5, n)
+        f32 = (rng.rand(n) < 0.5).astype(np.int32)
+        want = np.zeros(n, np.int32)
+        args = [np.ascontiguousarray(a, np.float64) for a in (px, py, vx, vy, r)]
+        L.cnref_norm_zone_violation(n, *[a.ctypes.data_as(ctypes.c_void_p) for a in args],
+                                    f32.ctypes.data_as(ctypes.c_void_p), lhs, want.ctypes.data_as(ctypes.c_void_p))
+        qx = np.zeros((n, 4)); qy = np.zeros((n, 4))
+        qx[:, 0], qy[:, 0], qx[:, 1], qy[:, 1] = vx, vy, f32, lhs
+        t = [torch.from_numpy(np.ascontiguousarray(a, np.float64)).to(dev) for a in (px, py, r, qx, qy)]
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        _lib.check(_lib.lib().cn_debug_disc_quad(ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream), n, 2,
+                                                 *[a.data_ptr() for a in t], out.data_ptr()))
+        got = out.cpu().numpy()
+        for i in np.nonzero(got != want)[0]:
+            m = L.cnref_norm_zone_margin(px[i], py[i], vx[i], vy[i], r[i], int(f32[i]), lhs)
+            assert abs(m) < (1e-6 if f32[i] else 1e-12), (lhs, i, m, got[i], want[i])
+            flips += 1
+        assert want.sum() > 100 and (want == 0).sum() > 100, want.mean()   # (true mostly on the 64-gon's axes)
+    assert flips <= 2 * n * 0.02, flips   # the on-axis headings (8 %) sit on the boundary by construction
