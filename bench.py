@@ -410,10 +410,13 @@ def run_c4(torch, dist, device, rank, world, E, N, K, W):
 
 
 def _barrier(torch, dist, device):
-    torch.cuda.synchronize(device)
+    # (device is the current device, torch.cuda.set_device in main: the plain synchronize skips the
+    # device-guard switch; one rank needs no second synchronize -- it ended a timed window with ~5 us of
+    # host overhead)
+    torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize(device)
+        torch.cuda.synchronize()
 
 
 def reset_total(eng):

@@ -48,9 +48,9 @@ def main(windows=8, K=20, W=5, E=4096):
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
         _lib.check(L.cn_profile_read(eng._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
         _lib.check(L.cn_profile(eng._h, 0, 0))
-        if w:   # the first window warms the bracket
-            walls.append(wall * 1e6)
-            spans.append(a.value * 1e3)
+        walls.append(wall * 1e6)   # (window 0 included: it shows the first window's extra cost)
+        spans.append(a.value * 1e3)
+    print("windows in order (wall / span us): " + ", ".join("%.0f/%.0f" % (a, b) for a, b in zip(walls, spans)))
     walls, spans = sorted(walls), sorted(spans)
     fixed = sorted(x - y for x, y in zip(walls, spans))
     print("%s: wall us median %.1f min %.1f | kernel span median %.1f | fixed median %.1f min %.1f | value median %.2f M"
