@@ -99,6 +99,21 @@ struct StepPlan {
 #ifndef CN_COVER_RANDGOAL
 #define CN_COVER_RANDGOAL 1   // diagnostic switch: the candidate-box cover for random goals on the circle
 #endif
+#ifndef CN_QUAD_PARK
+// the quad path's spawning waves park their spawns after a budget too (and cn_reset pre-draws the next two
+// spawns, as on the kd-tree path): round 6's timeline (stamps build without contended atomics) had the
+// spawn workgroups end last in 78 % of steady C2 launches, one circle_crossing spawn being ~82 k cycles
+#define CN_QUAD_PARK 1
+#endif
+#ifndef CN_QUAD_BUDGET
+#define CN_QUAD_BUDGET 70000   // clock cycles a quad-path spawning wave works per launch before parking
+#endif
+#ifndef CN_QUAD_SPAWN_WAVES
+#define CN_QUAD_SPAWN_WAVES 128   // spawning waves of the quad path's spare workgroups
+#endif
+#ifndef CN_SPAWN_PRIO
+#define CN_SPAWN_PRIO 0     // issue priority of the quad path's spawning waves (0: normal)
+#endif
 #ifndef CN_RNG_PRIO_ALL
 #define CN_RNG_PRIO_ALL 0   // diagnostic: raise the RNG waves' priority on the quad path too
 #endif
@@ -1205,7 +1220,7 @@ struct RngArgs {   // cn_reset_kernel
     PendPtrs pend;
     int E;
     int64_t counter_offset;
-    int draw_next;   // also draw the spawns of every env's next two resets (kd-tree path: PEND_FRESH)
+    int draw_next;   // also draw the spawns of every env's next two resets (then PEND_FRESH)
 };
 
 
@@ -2209,7 +2224,7 @@ __device__ __forceinline__ void goal_changes(const cn_config &c, const cn_state_
 
 // Auto-reset of env e (VecEnv worker, shmem_vec_env.py:164-168 -> CrowdSimDict.reset): copy the pending
 // spawn when `may_consume` and it is valid for the current key, else draw it here. One wave.
-template <bool GRID>
+template <bool GRID, bool FENCE = GRID>
 __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2, const cn_config &c, int64_t E, int64_t e,
                           int64_t counter_offset, bool may_consume, uint32_t launch_id, WRng &m, Env1 &en,
                           uint32_t *inline_count = nullptr)
@@ -2222,11 +2237,11 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2,
     const PendPtrs P = pend_slot(P2, rc & 1, E, E * N);
     // an entry completed by THIS launch (a resumed spawn finishing beside this reset) is not consumed: its
     // stores need not be visible yet; the reset draws inline instead. The key is read BEFORE ok, with an
-    // acquire fence between (GRID: the kd-tree path, the only one whose spawn waves resume parked spawns and
-    // may rewrite this slot during this launch; write_pending zeroes ok and fences before its key stores):
-    // a key written by this launch implies ok == 0 or this launch's id here.
+    // acquire fence between (FENCE: a path whose spawn waves resume parked spawns and may rewrite this slot
+    // during this launch; write_pending zeroes ok and fences before its key stores): a key written by this
+    // launch implies ok == 0 or this launch's id here.
     const bool key_ok = P.cc[e] == cc && P.rc[e] == rc;
-    if (GRID) __threadfence();
+    if (FENCE) __threadfence();
     const uint32_t ok = P.ok[e];
     if (may_consume && ok && ok != launch_id && key_ok) {
         if (lane < N) {
@@ -2279,36 +2294,37 @@ struct PendLaunch {
 };
 
 // GRID: the spawn's crowded rejection through a DiscGrid (the kd-tree path's plans have LDS for it).
-// Items: the envs reset by the previous launch (their spawn for the reset after next), then the spawns
+// PARK: spawns parked after the launch's budget and resumed later (the kd-tree path; the quad path with
+// CN_QUAD_PARK). Items: the envs reset by the previous launch (their spawn for the reset after next), then the spawns
 // the previous launch parked. With a budget, a wave parks its spawn between two humans once the budget
 // is spent (stream, robot and humans so far go to the pending slot, the item to rlist_w) and parks the
 // items it has not started; a later launch resumes them. The pending slot of a spawn is written only by
 // the wave that owns the item, and a reset consumes an entry only if an EARLIER launch completed it.
-template <bool PHX, bool GRID>
+template <bool PHX, bool GRID, bool PARK = GRID>
 __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_ptrs &S, const cn_config &c, int E, char *smem)
 {
     const int nw = pl.waves, w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (w >= nw) return;
+    if (!GRID && CN_SPAWN_PRIO) __builtin_amdgcn_s_setprio(CN_SPAWN_PRIO);
     const int N = c.human_num;
     char *base = smem + w * pl.stride;
     uint32_t *mtw = (uint32_t *)base;
     double *hb = (double *)(base + 2 * CN_MT_N * 4);
     // envs reset by the previous launch: the reset after next (the next one was drawn earlier); after
-    // cn_reset / cn_set_state (all): both the next (items [0, E)) and the one after ([E, 2E))
-    // (the quad path never sees PEND_FRESH: cn_reset's kernel pre-draws on the kd-tree path only)
-    const uint32_t nnew = (!GRID || pl.all == PEND_BOTH) && pl.all ? (uint32_t)(2 * E) : pl.all ? 0u : min(*pl.count, (uint32_t)E);
-    // parking / resuming exists on the kd-tree path only (GRID): the quad path's spawns are short, and
-    // its kernel keeps the plain loop (register pressure of the step path)
-    const uint32_t nres = (!GRID || pl.all) ? 0u : min(*pl.rcount, (uint32_t)(2 * E));
+    // cn_set_state (PEND_BOTH): both the next (items [0, E)) and the one after ([E, 2E)); after cn_reset
+    // (PEND_FRESH, its kernel pre-drew both): none
+    const uint32_t nnew = pl.all == PEND_BOTH ? (uint32_t)(2 * E) : pl.all ? 0u : min(*pl.count, (uint32_t)E);
+    // parked spawns of the previous launch (PARK)
+    const uint32_t nres = (!PARK || pl.all) ? 0u : min(*pl.rcount, (uint32_t)(2 * E));
     const int pb = pl.first ? (int)blockIdx.x : (int)blockIdx.x - pl.step_blocks;
-    const long long deadline = (GRID && pl.budget) ? (long long)clock64() + pl.budget : 0;
+    const long long deadline = (PARK && pl.budget) ? (long long)clock64() + pl.budget : 0;
     bool worked = false;   // a wave always works on its first item of the launch (progress for any budget)
     for (uint32_t it = (uint32_t)(pb * nw + w); it < nnew + nres; it += (uint32_t)(pl.pend_blocks * nw)) {
         int64_t e, cc;
         int32_t rc;
         bool started = false;
         if (it < nnew) {
-            const bool ahead2 = (GRID ? pl.all != PEND_BOTH : !pl.all) || it >= (uint32_t)E;
+            const bool ahead2 = pl.all != PEND_BOTH || it >= (uint32_t)E;
             // the key's counters come from a list entry, never from the state: the step workgroups of this
             // same launch reset terminal envs and rewrite reset_count / case_counter while the spawn waves run.
             // PEND_BOTH: cn_keysnap_kernel's snapshot of every env's counters, written (stream-ordered) by
@@ -2353,7 +2369,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
         double rth = 0;
         uint32_t ovf = 0;
         int sc = 0, i0 = 0;
-        if (GRID && started) {   // restore the parked spawn: stream at the park point, robot, the humans so far
+        if (PARK && started) {   // restore the parked spawn: stream at the park point, robot, the humans so far
             const PendPtrs P = pend_slot(pl.P, rc & 1, E, (int64_t)E * N);
             i0 = P.prog[e];
             const int nk = PHX ? 1 : CN_MT_N;
@@ -2380,10 +2396,10 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
                                          sc, i0, deadline);
         worked = true;
         const bool in1 = !m.phx && m.p > CN_MT_N;
-        write_pending<GRID>(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
+        write_pending<PARK>(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
                       lane, done == N ? pl.launch_id : 0u, done);
-        if (GRID && started && done == N && lane == 0) atomicAdd(pl.stats + 3, 1u);
-        if (GRID && done < N && lane == 0) {   // parked mid-way
+        if (PARK && started && done == N && lane == 0) atomicAdd(pl.stats + 3, 1u);
+        if (PARK && done < N && lane == 0) {   // parked mid-way
             atomicAdd(pl.stats + 1, 1u);
             const uint32_t k = atomicAdd(pl.rcount_w, 1u);
             if (k < (uint32_t)(2 * E)) {
@@ -2518,7 +2534,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
     if (sb < 0 || sb >= g.pend.step_blocks) {  // spare workgroups: draw upcoming episodes' spawns
         PendLaunch pl = g.pend;
         pl.ov = ov;
-        pend_waves<PHX, KD>(pl, g.s, c, g.E, smem);
+        pend_waves<PHX, KD, KD || CN_QUAD_PARK>(pl, g.s, c, g.E, smem);
         finish();
         return;
     }
@@ -3260,10 +3276,12 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                     if (l3) l3vis = lp3_replay<3>(R, Lb, cnt, fail_at, l3e, sl.vmax[h], sq, l3r + h * 12, l3k + h * 12, rx, ry);
 #ifdef CN_STAMPS
                     if (tid == 0 && (unsigned)sb < 4096) cn_stamp_a[sb * CN_NSTAMP + 23] = clock64() - tl3;
+#ifdef CN_STAMPS_LP3   // (two device-wide atomics per infeasible human: they slowed the stamps build by ~60 %)
                     if (l3 && sq == 0) {   // sub-problems solved / visited by RVO2's loop
                         atomicAdd(&cn_lp3_cnt[0], (unsigned long long)(l3e - fail_at));
                         atomicAdd(&cn_lp3_cnt[1], (unsigned long long)l3vis);
                     }
+#endif
 #else
                     (void)l3vis;
 #endif
@@ -3430,8 +3448,9 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             if (need & 1u) {
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
-                const bool may = KD ? g.pend.all != PEND_BOTH : !g.pend.all;   // ready unless this launch redraws both
-                reset_env<KD>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m, en, g.pend.stats + 7);
+                const bool may = g.pend.all != PEND_BOTH;   // ready unless this launch redraws both
+                reset_env<KD, KD || CN_QUAD_PARK>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m,
+                                                  en, g.pend.stats + 7);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
                     // the entry carries the counters this reset just wrote (its own stores, read back), so the
                     // next launch's spawn wave keys the spawn after next from them, never from a state that a
@@ -4193,7 +4212,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         const int64_t need = (E + nw - 1) / nw;
         // ~128 spawning waves on the quad path; 256 on the kd-tree path, whose crowded spawns (~1M cycles
         // each at 25 humans in square_crossing, ~4 % of the envs per step) must not queue behind each other
-        const int cap = (g->plan.kd ? 256 : 128) / nw;
+        const int cap = (g->plan.kd ? 256 : CN_QUAD_SPAWN_WAVES) / nw;
         const int pb = (int)(need < cap ? need : cap);
         g->pend_blocks = g->plan.kd ? (pb + 7) & ~7 : pb;   // leading: a multiple of 8 (XCD placement)
         // kd-tree path: a crowded spawn may take longer than the launch's step rounds; each spawning wave parks
@@ -4201,8 +4220,8 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         // later). Round 5: spawn-list entries carry the counters of the reset that queued them (a spawn wave
         // that read them from the state could see a later reset of the same env and queue a key that the next
         // launch queued again: two writers of one pending slot, one of them resuming from it -- 5 of 149 C3 runs
-        // departed; 0 of 149 with keyed entries). The quad path's spawns are short: never parked.
-        g->spawn_budget = 600000;
+        // departed; 0 of 149 with keyed entries). The quad path parks after CN_QUAD_BUDGET cycles (round 6).
+        g->spawn_budget = g->plan.kd ? 600000 : (CN_QUAD_PARK ? CN_QUAD_BUDGET : 0);
     }
     cn_state_bind(&g->s, g->state, g->E, g->N, cfg->robot_visible);
     if (circ_table_init() != hipSuccess) {
@@ -4402,10 +4421,10 @@ int cn_reset(cn_engine *g, void *stream, float *robot_node, float *temporal, flo
     a.o.case_size = g->case_size;
     a.o.ov.row = g->rows; a.o.ov.NS = g->NS;
     a.pend = g->pend; a.E = g->E; a.counter_offset = g->counter_offset;
-    // kd-tree path: the reset kernel draws the next two spawns too, so the first step launches (whose crowded
-    // spawns would otherwise run inline in step workgroups until the spawn waves catch up) find them drawn;
-    // the quad path's spawns are short and its first launch draws them (PEND_BOTH, as after cn_set_state)
-    a.draw_next = g->plan.kd ? 1 : 0;
+    // the reset kernel draws the next two spawns too, so the first step launches (whose spawns would otherwise
+    // run inline in step workgroups until the budgeted spawn waves catch up) find them drawn (PEND_FRESH);
+    // without quad-path parking the quad path's first launch draws them (PEND_BOTH, as after cn_set_state)
+    a.draw_next = (g->plan.kd || CN_QUAD_PARK) ? 1 : 0;
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
     hipLaunchKernelGGL(cn_reset_kernel, dim3(g->rng_grid), dim3(64), 0, st, a, g->c);
     HIPCHK(hipGetLastError());
@@ -4622,7 +4641,7 @@ int cn_debug_set_spawn_budget(cn_engine *g, long long cycles)
 {
     if (!g || cycles < 0) return set_err(CN_EINVAL, "cn_debug_set_spawn_budget: engine and cycles >= 0 required");
     for (int k = 0; k < g->ngroups; ++k) cn_debug_set_spawn_budget(g->grp[k], cycles);
-    if (!g->ngroups && g->plan.kd) g->spawn_budget = cycles;   // parking exists on the kd-tree path only
+    if (!g->ngroups && (g->plan.kd || CN_QUAD_PARK)) g->spawn_budget = cycles;   // (parking paths only)
     return CN_OK;
 }
 

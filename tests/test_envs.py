@@ -287,30 +287,38 @@ def test_step_seq_equals_single_steps():
             np.testing.assert_array_equal(a, b)
 
 
-def _c3_engine(E):
+def _c3_engine(E, shape="c3"):
     from crowdnav_dsrnn_amd.engine import CrowdNavEngine
 
     c = clone_config(Config())
-    c.sim.human_num = 25
     c.humans.policy = "orca"
-    c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
-    c.action_space.kinematics = "holonomic"
-    c.robot.FOV = c.humans.FOV = 1.0
+    if shape == "c3":
+        c.sim.human_num = 25
+        c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
+        c.action_space.kinematics = "holonomic"
+        c.robot.FOV = c.humans.FOV = 1.0
+    else:   # C2 (quad path)
+        c.sim.human_num = 10
+        c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+        c.action_space.kinematics = "unicycle"
     return CrowdNavEngine(make_cn_config(c, num_envs=E, nenv=E, phase="train"), "cuda:0")
 
 
 @pytest.mark.gpu
-def test_c3_first_launches_find_their_spawns_and_runs_repeat():
-    """The kd-tree path after cn_reset (C3 shape, 1024 envs x 25 humans, 60 launches): the reset kernel draws
-    every env's next two spawns, so no reset of the first launches draws a crowded spawn inline; and runs from
-    the same reset and actions end in the same state bit for bit, at the default spawn budget (spawns parked
-    and resumed at run-dependent points) and with the spawn waves parking after every human (20 k cycles)."""
-    E, T = 1024, 60
+@pytest.mark.parametrize("shape", ["c3", "c2"])
+def test_c3_first_launches_find_their_spawns_and_runs_repeat(shape):
+    """After cn_reset (C3 shape, 1024 envs x 25 humans, the kd-tree path; C2 shape, 4096 x 10, the quad path,
+    whose spawning waves park too since round 6; 60 launches): the reset kernel draws every env's next two
+    spawns, so no reset of the first launches draws a spawn inline; and runs from the same reset and actions
+    end in the same state bit for bit, at the default spawn budget (spawns parked and resumed at run-dependent
+    points) and with the spawn waves parking after every human (20 k cycles)."""
+    E, T = (1024, 60) if shape == "c3" else (4096, 60)
     g = torch.Generator(device="cuda:0").manual_seed(11)
-    acts = (torch.randn((T, E, 2), generator=g, device="cuda:0") * 0.5).contiguous()
+    acts = (torch.randn((T, E, 2), generator=g, device="cuda:0") * 0.5).contiguous() if shape == "c3" else \
+        (torch.rand((T, E, 2), generator=g, device="cuda:0") * 0.2 - 0.1).contiguous()
     blobs = []
     for budget in (None, None, 20000):
-        eng = _c3_engine(E)
+        eng = _c3_engine(E, shape)
         if budget is not None:
             eng.set_spawn_budget(budget)
         eng.reset()

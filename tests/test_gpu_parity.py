@@ -233,21 +233,23 @@ def _free_run_exact(ref, g, cfg, steps, kind, seed):
 
 
 def test_gpu_forced_spawn_parking_matches_oracle(gpu, oracle):
-    """The kd-tree path's resumable spawns under a 1-cycle budget: every spawning wave parks its spawn after
-    each human (at least one human per launch), so every upcoming episode is drawn over ~25 launches through
+    """Resumable spawns (the kd-tree path's and, since round 6, the quad path's) under a 1-cycle budget: every
+    spawning wave parks its spawn after each human (at least one human per launch), so every upcoming episode
+    is drawn over ~10-25 launches through
     the park / resume machinery (stored MT block and stream position, the robot and the humans so far,
     overflow count, scenario, Philox key), and resets that find their spawn unfinished draw inline. The
     rollout must equal the oracle exactly (done / event every step, state and every stream at the end), and
     the counters must show spawns parked mid-way, resumed and completed by a resume."""
-    for rngmode in ("mt19937", "philox"):
-        # 96 envs: fewer pending items than the 256 spawning waves, so every parked spawn is resumed by the
-        # next launch and completes ~25 launches after it started
-        cfg = _cfg(25, "holonomic", "square_crossing", E=96, fov=1.0, env__rng=rngmode)
+    for rngmode, shape in (("mt19937", "c3"), ("philox", "c3"), ("mt19937", "c2")):
+        # 96 envs: fewer pending items than the spawning waves, so every parked spawn is resumed by the
+        # next launch and completes ~25 (C3) / ~10 (C2, the quad path's parking, round 6) launches after it started
+        cfg = (_cfg(25, "holonomic", "square_crossing", E=96, fov=1.0, env__rng=rngmode) if shape == "c3" else
+               _cfg(10, "unicycle", E=96, env__rng=rngmode))
         ref, g = oracle.RefEngine(cfg), gpu(cfg)
         g.eng.set_spawn_budget(1)
         ref.reset()
         g.reset()
-        _free_run_exact(ref, g, cfg, 200, "holonomic", 17)
+        _free_run_exact(ref, g, cfg, 200, "holonomic" if shape == "c3" else "unicycle", 17)
         rs, gs = ref.get_state(), g.get_state()
         d = {"post_" + n: np.asarray(getattr(rs, n)) for n, _, _ in abi.STATE_FIELDS if n != "mt"}
         d["post_mt_crc"] = H.mt_crc(rs)
@@ -256,13 +258,13 @@ def test_gpu_forced_spawn_parking_matches_oracle(gpu, oracle):
         st = g.eng.spawn_stats()
         # (cn_reset draws every env's next two spawns itself, so the spawn waves' work starts at the third: 200
         # launches instead of round 4's 100 keep the resume path's coverage floor at 50 completions)
-        assert st["parked_midway"] > 1000 and st["resumed"] > 1000 and st["completed_on_resume"] > 50, (rngmode, st)
+        assert st["parked_midway"] > 1000 and st["resumed"] > 1000 and st["completed_on_resume"] > 50, (rngmode, shape, st)
 
 
 @pytest.mark.parametrize("shape,budget,start,tl", [
     ("c3", None, "reset", 1), ("c3", None, "set_state", 1), ("c3", None, "set_state", 2),
     ("c3", 1, "set_state", 1), ("c3", 1, "set_state", 2),
-    ("c2", None, "reset", 1), ("c2", None, "set_state", 1), ("c2", None, "set_state", 2),
+    ("c2", None, "reset", 1), ("c2", None, "set_state", 1), ("c2", None, "set_state", 2), ("c2", 1, "set_state", 2),
 ])
 def test_gpu_every_env_resets_every_launch(gpu, oracle, shape, budget, start, tl):
     """Spawn-key races. time_limit = 1 makes every env time out at its first step
@@ -275,10 +277,10 @@ def test_gpu_every_env_resets_every_launch(gpu, oracle, shape, budget, start, tl
     while the spawn waves key both pending slots; now keyed from cn_keysnap_kernel's snapshot). The state is
     re-loaded every 8 launches (from the oracle's), so a run holds eight draw-both launches. kd-tree path (C3
     shape; E = 1000, so an env's two items of a draw-both launch go to different spawning waves) at the default
-    spawn budget and at a 1-cycle budget (E = 192 < 256 spawning waves, so parked spawns are resumed), quad path
-    (C2 shape, 4096 envs); 64 launches each: done / event exact and rewards 1e-5 every launch, the whole state
+    spawn budget and at a 1-cycle budget (E = 192, so parked spawns are resumed), quad path (C2 shape, 4096 envs;
+    192 at a 1-cycle budget); 64 launches each: done / event exact and rewards 1e-5 every launch, the whole state
     and every MT19937 stream at the end."""
-    E = 4096 if shape == "c2" else (192 if budget == 1 else 1000)
+    E = 192 if budget == 1 else (4096 if shape == "c2" else 1000)
     if shape == "c3":
         cfg = _cfg(25, "holonomic", "square_crossing", E=E, fov=1.0, env__time_limit=tl)
     else:
@@ -310,7 +312,7 @@ def test_gpu_every_env_resets_every_launch(gpu, oracle, shape, budget, start, tl
     d["post_mt_crc"] = H.mt_crc(rs)
     errs = H.compare_state(gs, d, "post_", tol=1e-5)
     assert not errs, errs[:20]
-    if shape == "c3" and budget == 1:
+    if budget == 1:
         st = g.eng.spawn_stats()
         assert st["parked_midway"] > 0, st
         if tl == 2:   # at time_limit = 1 every wave's first item is a new spawn, so parked ones are never resumed
