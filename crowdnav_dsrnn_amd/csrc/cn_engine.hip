@@ -3436,6 +3436,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             for (int q = 0; q < nenv_here; ++q)
                 if (sl.rflag[EPB + q] & 7u) mine |= (jj++ % nw) == w;
         }
+        STAMP_T(22, 0);
         if (mine) {
         int j = 0;
         for (int q = 0; q < nenv_here; ++q) {

@@ -86,6 +86,24 @@ def run(variant, E=4096, N=10, steps=300):
     slow = tot >= np.percentile(tot, 95)
     print("  slowest 5%% workgroups (total >= %d): mean per phase %s" % (
         np.percentile(tot, 95), ", ".join("%s %d" % (nm.split()[0], d[slow, k].mean()) for k, nm in enumerate(names))))
+    # the slowest workgroups of the last launch: phases, and each env's phase-5 item (kind, cycles from the
+    # workgroup's phase-5 start; per-env stamps of the same workgroup share its XCD's clock)
+    Bx = b.reshape(-1, 24).astype(np.int64)
+    epb_ = 64 // N
+    nbk = len(tot)
+    xq, xr = nbk >> 3, nbk & 7
+    for k in np.argsort(-tot)[:8]:
+        items = []
+        xi = k & 7
+        blk = xi * xq + min(xi, xr) + (k >> 3)   # the kernel's XCD-aware env placement
+        for e in range(blk * epb_, min((blk + 1) * epb_, E)):
+            st_, rs, gl = Bx[e, 0], Bx[e, 5], Bx[e, 4]
+            if A[k, 5] <= st_ <= A[k, 6]:
+                kind = "reset" if A[k, 5] <= rs <= A[k, 6] and rs >= st_ else "goal"
+                end = rs if kind == "reset" else gl
+                items.append("%s %d-%d" % (kind, st_ - A[k, 5], end - A[k, 5]))
+        print("    WG %d total %d: %s | phase 5: wave 0 past its item count %d; %s" % (
+            k, tot[k], " ".join("%d" % d[k, j] for j in range(6)), A[k, 22] - A[k, 5], ", ".join(items) or "-"))
     span = A[:, 6].max() - A[:, 0].min()
     print("  launch span (first start -> last end) %d cycles; start skew max %d" % (span, A[:, 0].max() - A[:, 0].min()))
     # the whole grid on the device-wide 100 MHz clock (s_memtime above is per XCD: durations only)
