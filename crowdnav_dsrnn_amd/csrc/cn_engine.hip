@@ -111,6 +111,14 @@ struct StepPlan {
 #ifndef CN_QUAD_SPAWN_WAVES
 #define CN_QUAD_SPAWN_WAVES 128   // spawning waves of the quad path's spare workgroups
 #endif
+#ifndef CN_SLOT_FENCE
+// device-scope fences around the pending-slot handshake inside a step launch (write_pending / reset_env). On
+// gfx950 each is buffer_wbl2 sc1 + buffer_inv sc1: a write-back AND invalidation of the XCD's whole L2, once
+// per spawn written and per reset. Not needed (round 6, DESIGN §4 "Pending-slot fences"): within a launch no
+// reset reads a slot whose key that launch changes, and a slot's ok word is zeroed in an earlier launch than any
+// reset that could read it, so a reset sees ok == 0 or this launch's id for a slot being rewritten.
+#define CN_SLOT_FENCE 0
+#endif
 #ifndef CN_SPAWN_PRIO
 #define CN_SPAWN_PRIO 0     // issue priority of the quad path's spawning waves (0: normal)
 #endif
@@ -2396,7 +2404,7 @@ __device__ __forceinline__ void pend_waves(const PendLaunch &pl, const cn_state_
                                          sc, i0, deadline);
         worked = true;
         const bool in1 = !m.phx && m.p > CN_MT_N;
-        write_pending<PARK>(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
+        write_pending<PARK && CN_SLOT_FENCE>(pl.P, c, E, e, en, rth, sc, ovf, m.blk(in1 ? 1 : 0), in1 ? m.p - CN_MT_N : m.p, cc, rc,
                       lane, done == N ? pl.launch_id : 0u, done);
         if (PARK && started && done == N && lane == 0) atomicAdd(pl.stats + 3, 1u);
         if (PARK && done < N && lane == 0) {   // parked mid-way
@@ -3450,7 +3458,8 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
                 const bool may = g.pend.all != PEND_BOTH;   // ready unless this launch redraws both
-                reset_env<KD, KD || CN_QUAD_PARK>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may, g.pend.launch_id, m,
+                reset_env<KD, (KD || CN_QUAD_PARK) && CN_SLOT_FENCE>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may,
+                                                                     g.pend.launch_id, m,
                                                   en, g.pend.stats + 7);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
                     // the entry carries the counters this reset just wrote (its own stores, read back), so the
