@@ -112,11 +112,10 @@ struct StepPlan {
 #define CN_QUAD_SPAWN_WAVES 128   // spawning waves of the quad path's spare workgroups
 #endif
 #ifndef CN_SLOT_FENCE
-// device-scope fences around the pending-slot handshake inside a step launch (write_pending / reset_env). On
-// gfx950 each is buffer_wbl2 sc1 + buffer_inv sc1: a write-back AND invalidation of the XCD's whole L2, once
-// per spawn written and per reset. Not needed (round 6, DESIGN §4 "Pending-slot fences"): within a launch no
-// reset reads a slot whose key that launch changes, and a slot's ok word is zeroed in an earlier launch than any
-// reset that could read it, so a reset sees ok == 0 or this launch's id for a slot being rewritten.
+// device-scope fences around the pending-slot handshake inside a step launch (write_pending / reset_env), the
+// round-5 protocol (ok zeroed and fenced before a slot's new key; key, fence, ok on the reader's side). On gfx950
+// each is buffer_wbl2 sc1 + buffer_inv sc1: a write-back AND invalidation of the XCD's whole L2, once per spawn
+// written and per reset. Round 6 replaces them by a key-tagged ok word (PendPtrs::ok, reset_env), which needs none.
 #define CN_SLOT_FENCE 0
 #endif
 #ifndef CN_SPAWN_PRIO
@@ -1181,7 +1180,8 @@ struct PendPtrs {
     int32_t *sc;    // [E] scenario
     int64_t *cc;    // [E] key: case_counter the spawn was drawn for
     int32_t *rc;    // [E] key: reset_count (sequential scenario mode)
-    uint32_t *ok;   // [E] 0, or the id of the launch that completed the entry (consumed only by a LATER launch)
+    uint64_t *ok;   // [E] (reset_count key << 32) | id of the launch that completed the entry (0: parked / none);
+                    // one 8-byte store, written last: consumed only by a LATER launch, and only for its own key
     int32_t *prog;  // [E] humans placed so far by a spawn parked mid-way (resumable spawns)
     double *r;      // [5][E] robot px, py, gx, gy, theta
     double *h;      // [7][E*N] human px, py, gx, gy, radius, v_pref, theta
@@ -1909,9 +1909,8 @@ __device__ __forceinline__ int spawn_env(const cn_config &c, int64_t gidx, int64
 // Store a drawn spawn as env e's pending episode for the reset with key (cc, rc), slot rc & 1.
 // okv: the completing launch's id, or 0 with `prog` = humans placed for a spawn parked mid-way (the
 // stream at the park point, the robot and the first prog humans are stored; resumed by a later launch).
-// FENCE: the kd-tree path, whose spawn waves resume parked spawns and may rewrite a slot that a reset of the
-// same launch reads (the quad path only ever writes the slot of the reset after next: no fences there, each
-// is a write-back of the XCD's L2)
+// FENCE: the round-5 handshake (CN_SLOT_FENCE); the ok word, written last, carries the entry's key and the
+// completing launch's id, which is all a reset of a later launch needs (reset_env)
 template <bool FENCE>
 __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_config &c, int64_t E, int64_t e, const Env1 &en, double rth,
                               int sc, uint32_t ovf, const uint32_t *mt_src, int pos, int64_t cc, int32_t rc, int lane,
@@ -1924,7 +1923,7 @@ __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_confi
     // a reset of the same launch that reads the slot (reset_env: key, fence, then ok) and sees a new key
     // then sees ok == 0 (or this launch's id) and draws inline instead of reading a half-written payload.
     if (FENCE) {
-        if (lane == 0) P.ok[e] = 0u;
+        if (lane == 0) P.ok[e] = 0ull;
         __threadfence();
     }
     {
@@ -1946,7 +1945,7 @@ __device__ __forceinline__ void write_pending(const PendPtrs &P2, const cn_confi
         P.prog[e] = okv ? 0 : prog;
     }
     if (FENCE) __threadfence();   // the whole entry before its ok word (release)
-    if (lane == 0) P.ok[e] = okv;
+    if (lane == 0) P.ok[e] = ((uint64_t)(uint32_t)rc << 32) | okv;
 }
 
 // The deterministic rest of CrowdSimDict.reset (crowd_sim_dict.py:136-203): state of the new episode,
@@ -2243,14 +2242,16 @@ __device__ __forceinline__ void reset_env(const ResetOut &o, const PendPtrs &P2,
     const int64_t cc = S.case_counter[e];
     const int32_t rc = S.reset_count[e];
     const PendPtrs P = pend_slot(P2, rc & 1, E, E * N);
-    // an entry completed by THIS launch (a resumed spawn finishing beside this reset) is not consumed: its
-    // stores need not be visible yet; the reset draws inline instead. The key is read BEFORE ok, with an
-    // acquire fence between (FENCE: a path whose spawn waves resume parked spawns and may rewrite this slot
-    // during this launch; write_pending zeroes ok and fences before its key stores): a key written by this
-    // launch implies ok == 0 or this launch's id here.
-    const bool key_ok = P.cc[e] == cc && P.rc[e] == rc;
+    // An entry completed by THIS launch (a resumed spawn finishing beside this reset) is not consumed: its
+    // stores need not be visible yet; the reset draws inline instead.
+    // The ok word carries the key it completes and is read first: only an entry completed by an earlier launch
+    // FOR THIS KEY is consumed, and no wave of this launch writes such a slot (a slot is rewritten for key rc + 2
+    // only after this reset; a spawn of key rc that is written for the first time in this very launch shows the
+    // key in its ok word only with id 0 or this launch's), so the payload read after it needs no fence.
+    const uint64_t okw = P.ok[e];
+    const uint32_t ok = (uint32_t)okw;
     if (FENCE) __threadfence();
-    const uint32_t ok = P.ok[e];
+    const bool key_ok = (int32_t)(uint32_t)(okw >> 32) == rc && P.cc[e] == cc && P.rc[e] == rc;
     if (may_consume && ok && ok != launch_id && key_ok) {
         if (lane < N) {
             const int64_t h = e * N + lane, EN = E * N;
@@ -4179,7 +4180,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
     // pending spawns: every array holds both slots ([2][...], pend_slot)
     const int64_t pb_mt = al(2 * E * CN_MT_N * 4), pb_i = al(2 * E * 4), pb_cc = al(2 * E * 8), pb_r = al(2 * 5 * E * 8),
                   pb_h = al(2 * 7 * EN * 8);
-    const int64_t pend_bytes = pb_mt + 6 * pb_i + pb_cc + pb_r + pb_h;
+    const int64_t pend_bytes = pb_mt + 5 * pb_i + 2 * pb_cc + pb_r + pb_h;
     hipError_t e1 = hipMalloc(&g->state, g->state_bytes);
     hipError_t e2 = hipMalloc(&g->work, sizeof(uint32_t) * (g->E + 64));
     hipError_t e3 = hipMalloc(&g->work_count, 64);
@@ -4205,7 +4206,7 @@ int cn_create(const cn_config *cfg, int device, cn_engine **out)
         g->pend.ovf = (uint32_t *)b; b += pb_i;
         g->pend.sc = (int32_t *)b; b += pb_i;
         g->pend.rc = (int32_t *)b; b += pb_i;
-        g->pend.ok = (uint32_t *)b; b += pb_i;
+        g->pend.ok = (uint64_t *)b; b += pb_cc;
         g->pend.prog = (int32_t *)b; b += pb_i;
         g->pend.cc = (int64_t *)b; b += pb_cc;
         g->pend.r = (double *)b; b += pb_r;

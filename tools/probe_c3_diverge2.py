@@ -2,7 +2,7 @@
 every later run compares at the same launches and, at the first difference, prints the launch, the envs and
 the differing fields with both runs' values for the first envs.
 
-    python tools/probe_c3_diverge2.py [R] [K] [S] [spawn budget]
+    python tools/probe_c3_diverge2.py [R] [K] [S] [spawn budget] [c3|c2]
 """
 import os
 import sys
@@ -16,13 +16,21 @@ from crowdnav_dsrnn_amd.config import Config, clone_config, make_cn_config  # no
 from crowdnav_dsrnn_amd.engine import CrowdNavEngine  # noqa: E402
 
 
+WL = "c3"
+
+
 def make(E=4096, N=25):
     c = clone_config(Config())
-    c.sim.human_num = N
     c.humans.policy = "orca"
-    c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
-    c.action_space.kinematics = "holonomic"
-    c.robot.FOV = c.humans.FOV = 1.0
+    if WL == "c2":   # the quad path (its spawns park too since round 6)
+        N = 10
+        c.sim.train_val_sim = c.sim.test_sim = ["circle_crossing"]
+        c.action_space.kinematics = "unicycle"
+    else:
+        c.sim.train_val_sim = c.sim.test_sim = ["square_crossing"]
+        c.action_space.kinematics = "holonomic"
+        c.robot.FOV = c.humans.FOV = 1.0
+    c.sim.human_num = N
     return CrowdNavEngine(make_cn_config(c, num_envs=E, nenv=E, phase="train"), "cuda:0"), E, N
 
 
@@ -37,7 +45,8 @@ def main(R=12, K=400, S=10, budget=None):
         eng.reset()
         found = False
         for s in range(K):
-            eng.step(torch.randn((E, 2), generator=g, device="cuda:0") * 0.5)
+            eng.step(torch.randn((E, 2), generator=g, device="cuda:0") * 0.5 if WL == "c3" else
+                     torch.rand((E, 2), generator=g, device="cuda:0") * 0.2 - 0.1)
             if (s + 1) % S:
                 continue
             sv = eng.get_state()
@@ -47,7 +56,7 @@ def main(R=12, K=400, S=10, budget=None):
             b0 = ref[(s + 1) // S - 1]
             if np.array_equal(b0, np.asarray(sv.blob)):
                 continue
-            s0 = abi.StateView(b0, E, N, 0)
+            s0 = abi.StateView(b0, E, N, 0)   # (robot not visible in either workload)
             diff = {}
             for n, _, _ in abi.STATE_FIELDS:
                 a0 = np.asarray(getattr(s0, n)).reshape(E, -1)
@@ -72,4 +81,6 @@ def main(R=12, K=400, S=10, budget=None):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 5:
+        WL = sys.argv[5]
     main(*(int(x) for x in sys.argv[1:5]))
