@@ -3956,43 +3956,55 @@ __device__ int kd_neighbors_seq(int A, const float *X, const float *Y, uint8_t *
     return cnt;
 }
 
+// LDS of one cn_orca_kd_kernel workgroup, sized by the simulators' agent count A (dynamic): 16 quads' lines
+// and projected lines [A - 1] float4 each, positions [A] float x 2, agents_ order and neighbours [A] bytes, counts.
+// (Sized for CN_ORCA_MAXA it was 42.5 KB, 3 one-wave workgroups per CU; at A = 26, 17 KB: 9.)
+__host__ __device__ inline int orca_kd_lds(int A)
+{
+    return 16 * (2 * 16 * (A - 1) + 2 * 4 * A) + ((2 * 16 * A + 15) & ~15) + 16 * 4;
+}
+
 __global__ void __launch_bounds__(64) cn_orca_kd_kernel(int64_t n, int A, const float *__restrict__ ag,
                                                         const float *__restrict__ self, float nd, float th, float ts,
                                                         uint8_t *__restrict__ perm_io, float *__restrict__ out)
 {
-    __shared__ float4 Ls[16][CN_ORCA_MAXA - 1], Ps[16][CN_ORCA_MAXA - 1];
-    __shared__ float Xs[16][CN_ORCA_MAXA], Ys[16][CN_ORCA_MAXA];
-    __shared__ uint8_t Pm[16][CN_ORCA_MAXA], Nb[16][CN_ORCA_MAXA];
-    __shared__ int Cn[16];
+    extern __shared__ __attribute__((aligned(16))) char kd_smem[];
     const int q = threadIdx.x >> 2, sq = threadIdx.x & 3;
+    float4 *Lq = (float4 *)kd_smem + q * (A - 1);                 // [16][A - 1]
+    float4 *Pq = (float4 *)kd_smem + 16 * (A - 1) + q * (A - 1);  // [16][A - 1]
+    float *Xq = (float *)(kd_smem + 16 * 2 * 16 * (A - 1)) + q * A;
+    float *Yq = (float *)(kd_smem + 16 * 2 * 16 * (A - 1)) + 16 * A + q * A;
+    uint8_t *Pmq = (uint8_t *)(kd_smem + 16 * (2 * 16 * (A - 1) + 2 * 4 * A)) + q * A;
+    uint8_t *Nbq = (uint8_t *)(kd_smem + 16 * (2 * 16 * (A - 1) + 2 * 4 * A)) + 16 * A + q * A;
+    int *Cn = (int *)(kd_smem + orca_kd_lds(A) - 16 * 4);
     const int64_t i = (int64_t)blockIdx.x * 16 + q;
     const bool act = i < n;
     const float *a = ag + (act ? i : 0) * A * 5;
     if (act)
         for (int k = sq; k < A; k += 4) {
-            Xs[q][k] = a[k * 5]; Ys[q][k] = a[k * 5 + 1];
-            Pm[q][k] = perm_io ? perm_io[i * A + k] : (uint8_t)k;
+            Xq[k] = a[k * 5]; Yq[k] = a[k * 5 + 1];
+            Pmq[k] = perm_io ? perm_io[i * A + k] : (uint8_t)k;
         }
     wsync();
-    if (act && sq == 0) Cn[q] = A > 1 ? kd_neighbors_seq(A, Xs[q], Ys[q], Pm[q], nd * nd, Nb[q]) : 0;
+    if (act && sq == 0) Cn[q] = A > 1 ? kd_neighbors_seq(A, Xq, Yq, Pmq, nd * nd, Nbq) : 0;
     wsync();
     if (act) {
         const int cnt = Cn[q];
         const float invTH = fdiv(1.0f, th), invTS = fdiv(1.0f, ts);
         for (int k = sq; k < cnt; k += 4) {
-            const float *o = a + Nb[q][k] * 5;
-            Ls[q][k] = orca_line(a[0], a[1], a[2], a[3], a[4], o[0], o[1], o[2], o[3], o[4], invTH, invTS);
+            const float *o = a + Nbq[k] * 5;
+            Lq[k] = orca_line(a[0], a[1], a[2], a[3], a[4], o[0], o[1], o[2], o[3], o[4], invTH, invTS);
         }
         if (perm_io)
-            for (int k = sq; k < A; k += 4) perm_io[i * A + k] = Pm[q][k];
+            for (int k = sq; k < A; k += 4) perm_io[i * A + k] = Pmq[k];
     }
     wsync();
     if (act) {
         const int cnt = Cn[q];
         const float vmax = self[3 * i], ox = self[3 * i + 1], oy = self[3 * i + 2];
         float rx, ry;
-        const int fail_at = lp2_q<uint64_t>(Ls[q], cnt, vmax, ox, oy, sq, rx, ry);
-        if (fail_at < cnt) lp3_q<uint64_t>(Ls[q], Ps[q], cnt, fail_at, vmax, sq, rx, ry);
+        const int fail_at = lp2_q<uint64_t>(Lq, cnt, vmax, ox, oy, sq, rx, ry);
+        if (fail_at < cnt) lp3_q<uint64_t>(Lq, Pq, cnt, fail_at, vmax, sq, rx, ry);
         if (sq == 0) {
             out[4 * i] = rx; out[4 * i + 1] = ry; out[4 * i + 2] = (float)fail_at; out[4 * i + 3] = (float)cnt;
         }
@@ -4730,8 +4742,8 @@ int cn_orca_predict_kd(void *stream, int64_t n, int A, const float *agents, cons
     if (n <= 0 || !agents || !self || !out) return set_err(CN_EINVAL, "cn_orca_predict_kd: n > 0 and buffers required");
     if (A < 1 || A > CN_ORCA_MAXA) return set_err(CN_EUNSUPPORTED, "cn_orca_predict_kd: 1 <= A <= 64");
     (void)hipGetLastError();   // a stale error of an earlier call (any library) is not this launch's
-    hipLaunchKernelGGL(cn_orca_kd_kernel, dim3((unsigned)((n + 15) / 16)), dim3(64), 0, (hipStream_t)stream, n, A,
-                       agents, self, neighbor_dist, time_horizon, time_step, perm, out);
+    hipLaunchKernelGGL(cn_orca_kd_kernel, dim3((unsigned)((n + 15) / 16)), dim3(64), orca_kd_lds(A), (hipStream_t)stream,
+                       n, A, agents, self, neighbor_dist, time_horizon, time_step, perm, out);
     HIPCHK(hipGetLastError());
     return CN_OK;
 }
