@@ -152,7 +152,7 @@ __host__ __device__ inline StepPlan cn_step_plan(int N, int robot_visible)
     int o = 0;
     p.o_renv = o;  o = cn_align16(o + CN_RENV_F * p.EPB * 8);
     p.o_racts = o; o = cn_align16(o + 2 * p.EPB * 4);
-    p.o_rflag = o; o = cn_align16(o + 3 * p.EPB * 4);
+    p.o_rflag = o; o = cn_align16(o + (3 * p.EPB + 2) * 4);   // + the 64-bit mask of envs with RNG work
     p.o_rvr = o;   o = cn_align16(o + 8 * p.EPB * 8);
     p.o_hum = o;   o = cn_align16(o + CN_HUM_F * H * 8);
     p.o_lane = o;  o = cn_align16(o + H * 8 + H * 4);      // closest distance (f64) + flag word
@@ -3413,6 +3413,10 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
         const bool egoal = c.end_goal_changing && endg;
         sl.rflag[EPB + re] = (done ? 1u : 0u) | (rgoal ? 2u : 0u) | (egoal ? 4u : 0u);
     }
+    if ((tid >> 6) == 1) {   // the env lanes' wave: one mask of the envs with RNG work, for phase 5's item split
+        const uint64_t bm = __ballot(rl && (sl.rflag[EPB + re] & 7u) != 0u);
+        if (tid == 64) { sl.rflag[3 * EPB] = (uint32_t)bm; sl.rflag[3 * EPB + 1] = (uint32_t)(bm >> 32); }
+    }
     __syncthreads();
     STAMP_A(4);
     STAMP_A(5);
@@ -3438,20 +3442,22 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
         o.s = S; o.robot_node = g.robot_node; o.temporal = g.temporal; o.spatial = g.spatial; o.case_size = g.case_size;
         o.ov = ov;
         // waves without an env to serve skip the block entirely: the loop's preheader (values the
-        // compiler hoists out of the RNG work, and their spill stores) then runs only where it is needed
-        bool mine = false;
+        // compiler hoists out of the RNG work, and their spill stores) then runs only where it is needed.
+        // The envs with work, in env order, go round-robin to the RNG waves: this wave's share from the mask
+        // wave 1 wrote (scalar bit loop, one LDS read instead of a dependent chain over the envs' flags)
+        const uint64_t rm = ((uint64_t)__builtin_amdgcn_readfirstlane(sl.rflag[3 * EPB + 1]) << 32) |
+                            (uint64_t)__builtin_amdgcn_readfirstlane(sl.rflag[3 * EPB]);
+        uint64_t mym = 0;
         {
             int jj = 0;
-            for (int q = 0; q < nenv_here; ++q)
-                if (sl.rflag[EPB + q] & 7u) mine |= (jj++ % nw) == w;
+            for (uint64_t mm = rm; mm; mm &= mm - 1, ++jj)
+                if (jj % nw == w) mym |= mm & (~mm + 1);
         }
         STAMP_T(22, 0);
-        if (mine) {
-        int j = 0;
-        for (int q = 0; q < nenv_here; ++q) {
+        if (mym) {
+        for (uint64_t mm = mym; mm; mm &= mm - 1) {
+            const int q = __builtin_ctzll(mm);
             const uint32_t need = sl.rflag[EPB + q] & 7u;
-            if (!need) continue;
-            if ((j++ % nw) != w) continue;
             const int64_t e = e0 + q;
             STAMP_B(e, 0);
             Env1 en;
