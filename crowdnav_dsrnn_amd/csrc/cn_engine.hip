@@ -2456,6 +2456,11 @@ struct StepArgs {
     double cth_h, cth_r;    // cos(human_fov / 2), cos(robot_fov / 2): in_fov's thresholds
 };
 
+// phase 5 reads cn_config from the kernarg segment right after StepArgs (cn_step_kernel's RNG loop): the
+// by-value arguments are laid out in order at their natural alignment (AMDHSA metadata: 0 / 720 today)
+static_assert(alignof(StepArgs) >= alignof(cn_config) || sizeof(StepArgs) % alignof(cn_config) == 0,
+              "cn_step_kernel's kernarg layout: cn_config follows StepArgs");
+
 // observed agent of slot k seen by lane (human i of env base eb): position/velocity float32,
 // frozen RVO2 radius; `vis` = visible now, `dm` = dummy at simulator creation
 __device__ inline void slot_agent(const SL &sl, const cn_config &c, int eb, int el, int EPB, int N, int i, int k,
@@ -3438,9 +3443,6 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
         // the RNG waves' goal loops end most of the slowest workgroups (kd-tree path): issue priority over
         // the other workgroups' waves on their SIMD (C3 460.3 / 461.6 -> 456.8 / 456.4 us per launch, A/B)
         if ((KD || CN_RNG_PRIO_ALL) && w < nw) __builtin_amdgcn_s_setprio(3);
-        ResetOut o;
-        o.s = S; o.robot_node = g.robot_node; o.temporal = g.temporal; o.spatial = g.spatial; o.case_size = g.case_size;
-        o.ov = ov;
         // waves without an env to serve skip the block entirely: the loop's preheader (values the
         // compiler hoists out of the RNG work, and their spill stores) then runs only where it is needed.
         // The envs with work, in env order, go round-robin to the RNG waves: this wave's share from the mask
@@ -3457,6 +3459,23 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
         if (mym) {
         for (uint64_t mm = mym; mm; mm &= mm - 1) {
             const int q = __builtin_ctzll(mm);
+            // the kernel arguments through pointers the compiler cannot see across iterations: their loads stay at
+            // the uses in this body instead of a preheader that reloaded ~30 of them one by one and parked ~250
+            // SGPR values in VGPR lanes before the first item (~4 k cycles on the slowest workgroups)
+            // (read from the kernarg segment itself: taking the parameters' addresses would copy them to scratch;
+            // by-value arguments in order at their natural alignment, StepArgs at 0, cn_config after it)
+            typedef const __attribute__((address_space(4))) char *KArgs;
+            typedef const __attribute__((address_space(4))) StepArgs *GArgs;
+            typedef const __attribute__((address_space(4))) cn_config *CArgs;
+            KArgs ks = (KArgs)__builtin_amdgcn_kernarg_segment_ptr();
+            asm volatile("" : "+s"(ks));
+            GArgs gq = (GArgs)ks;
+            CArgs cq = (CArgs)(ks + ((sizeof(StepArgs) + alignof(cn_config) - 1) & ~(alignof(cn_config) - 1)));
+            const StepArgs &G = *(const StepArgs *)gq;
+            const cn_config &C = *(const cn_config *)cq;
+            ResetOut o;
+            o.s = G.s; o.robot_node = G.robot_node; o.temporal = G.temporal; o.spatial = G.spatial;
+            o.case_size = G.case_size; o.ov = ov;
             const uint32_t need = sl.rflag[EPB + q] & 7u;
             const int64_t e = e0 + q;
             STAMP_B(e, 0);
@@ -3464,19 +3483,18 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             if (need & 1u) {
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
-                const bool may = g.pend.all != PEND_BOTH;   // ready unless this launch redraws both
-                reset_env<KD, (KD || CN_QUAD_PARK) && CN_SLOT_FENCE>(o, g.pend.P, c, g.E, e, g.pend.counter_offset, may,
-                                                                     g.pend.launch_id, m,
-                                                  en, g.pend.stats + 7);
+                const bool may = G.pend.all != PEND_BOTH;   // ready unless this launch redraws both
+                reset_env<KD, (KD || CN_QUAD_PARK) && CN_SLOT_FENCE>(o, G.pend.P, C, G.E, e, G.pend.counter_offset, may,
+                                                                     G.pend.launch_id, m, en, G.pend.stats + 7);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
                     // the entry carries the counters this reset just wrote (its own stores, read back), so the
                     // next launch's spawn wave keys the spawn after next from them, never from a state that a
                     // later reset of the same env may be rewriting while it reads
-                    const int64_t ccn = S.case_counter[e];
-                    const int32_t rcn = S.reset_count[e];
-                    const uint32_t k = atomicAdd(g.pcount_w, 1u);
-                    if (k < (uint32_t)g.E) {
-                        uint32_t *q = g.plist_w + 4 * k;
+                    const int64_t ccn = G.s.case_counter[e];
+                    const int32_t rcn = G.s.reset_count[e];
+                    const uint32_t k = atomicAdd(G.pcount_w, 1u);
+                    if (k < (uint32_t)G.E) {
+                        uint32_t *q = G.plist_w + 4 * k;
                         q[0] = (uint32_t)e; q[1] = (uint32_t)rcn;
                         q[2] = (uint32_t)(uint64_t)ccn; q[3] = (uint32_t)((uint64_t)ccn >> 32);
                     }
@@ -3491,7 +3509,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                 // update_human_goal checks every human AFTER the random changes (a new random goal may
                 // land within reach of its own human), so it runs whenever end goal changing is on
                 m.edbg = e;
-                goal_changes<KD>(c, S, e, en, m, (need & 2u) != 0, c.end_goal_changing != 0, hb);
+                goal_changes<KD>(C, G.s, e, en, m, (need & 2u) != 0, C.end_goal_changing != 0, hb);
             }
         }
         }
