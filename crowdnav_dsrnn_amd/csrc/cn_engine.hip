@@ -3483,18 +3483,21 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             if (need & 1u) {
                 en.hpx = hb; en.hpy = hb + 32; en.hgx = hb + 64; en.hgy = hb + 96; en.hr = hb + 128; en.hvp = hb + 160;
                 en.hth = hb + 192;
-                const bool may = G.pend.all != PEND_BOTH;   // ready unless this launch redraws both
+                // (pend.all, pend.launch_id, pcount_w and plist_w from the kernel's own copy g: graph mode (DEVSEQ)
+                // rewrote them at the top from the device-side step counter; the kernarg segment holds the values of
+                // the captured launch)
+                const bool may = g.pend.all != PEND_BOTH;   // ready unless this launch redraws both
                 reset_env<KD, (KD || CN_QUAD_PARK) && CN_SLOT_FENCE>(o, G.pend.P, C, G.E, e, G.pend.counter_offset, may,
-                                                                     G.pend.launch_id, m, en, G.pend.stats + 7);
+                                                                     g.pend.launch_id, m, en, G.pend.stats + 7);
                 if (lane == 0) {   // each env resets at most once per launch: k < E (guarded all the same)
                     // the entry carries the counters this reset just wrote (its own stores, read back), so the
                     // next launch's spawn wave keys the spawn after next from them, never from a state that a
                     // later reset of the same env may be rewriting while it reads
                     const int64_t ccn = G.s.case_counter[e];
                     const int32_t rcn = G.s.reset_count[e];
-                    const uint32_t k = atomicAdd(G.pcount_w, 1u);
+                    const uint32_t k = atomicAdd(g.pcount_w, 1u);
                     if (k < (uint32_t)G.E) {
-                        uint32_t *q = G.plist_w + 4 * k;
+                        uint32_t *q = g.plist_w + 4 * k;
                         q[0] = (uint32_t)e; q[1] = (uint32_t)rcn;
                         q[2] = (uint32_t)(uint64_t)ccn; q[3] = (uint32_t)((uint64_t)ccn >> 32);
                     }

@@ -364,3 +364,47 @@ def test_full_size_runs_repeat_bit_for_bit(shape, budget):
             ref = blob
         else:
             np.testing.assert_array_equal(blob, ref, err_msg="run %d departs from run 0" % r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["c2", "c3"])
+def test_graph_mode_replays_equal_eager_with_spawns_drawn_ahead(shape):
+    """Graph mode (cn_set_graph_mode: the step sequence, spawn-list indices and launch ids live on the device):
+    a HIP graph of 16 cn_step launches replayed 12 times equals 192 eager launches bit for bit, AND the spawns
+    stay drawn ahead -- no more resets drawn inline than the eager run. The replayed launches' kernel arguments
+    are those of the captured launches; a kernel reading the spawn-list pointers, the launch id or the draw-both
+    flag from its arguments instead of the device-derived copy would queue the spawns into a stale list (every
+    reset then drawn inline, results still equal) or accept a pending entry completed by its own launch."""
+    E = 1024 if shape == "c3" else 4096
+    T, R = 16, 12
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    acts = (torch.randn((T * R + 1, E, 2), generator=g, device="cuda:0") * 0.5).contiguous() if shape == "c3" else \
+        (torch.rand((T * R + 1, E, 2), generator=g, device="cuda:0") * 0.2 - 0.1).contiguous()
+    out = []
+    for graph in (False, True):
+        eng = _c3_engine(E, shape)
+        eng.reset()
+        eng.step(acts[0])   # (one eager launch before the capture, as RolloutTrainer's warm-up does)
+        st0 = eng.spawn_stats()
+        if graph:
+            buf = acts[1:1 + T].clone()
+            eng.set_graph_mode(True)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                for t in range(T):
+                    eng.step(buf[t])
+            eng.set_graph_mode(False)   # (recorded, not run: the device sequence is unchanged)
+            eng.set_graph_mode(True)
+            for r in range(R):
+                buf.copy_(acts[1 + r * T:1 + (r + 1) * T])
+                gr.replay()
+            torch.cuda.synchronize()
+            eng.set_graph_mode(False)
+        else:
+            for t in range(T * R):
+                eng.step(acts[1 + t])
+        st = eng.spawn_stats()
+        out.append((np.asarray(eng.get_state().blob).copy(), st["inline_resets"] - st0["inline_resets"]))
+        eng.close()
+    assert out[1][1] <= out[0][1] + 2, (out[0][1], out[1][1])
+    np.testing.assert_array_equal(out[0][0], out[1][0])
