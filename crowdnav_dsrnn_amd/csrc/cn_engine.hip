@@ -2834,6 +2834,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
     // distances / flags and the robot-only terms), so it runs inside phase 2 on the env lanes (wave 1, after
     // its own ORCA quads), in the slack while the slowest humans finish their linear programs. The robot's
     // kinematics update (which the ORCA simulators must not see yet) is applied after phase 2.
+    bool ladder_done = false;   // the quad ORCA path runs it inside phase 2 (before the linearProgram3 tasks)
     auto ladder = [&]() {
         const double rr = RF(sl, R_RAD, re, EPB);
         const uint32_t flags = sl.rflag[re];
@@ -3280,6 +3281,15 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
                     const bool l3 = hq && fail_at < cnt;
                     const int l3e = min(cnt, fail_at + CN_LP3_W);
                     if (sq == 0) l3b[h] = l3 ? (uint32_t)(fail_at | (l3e << 8)) : 0u;
+                    // the calc_reward ladder here, while the waves wait for the slowest linearProgram2 at this
+                    // barrier (after the linear programs it was the last item of its wave's phase 2: stamps of the
+                    // driver's window put it at ~5 k of the slowest workgroups' ~63 k phase-2 cycles). It reads only
+                    // phase-1 results and writes no value the linear programs or human_post read. Not with norm
+                    // zones: their separating-axis tests make the ladder longer than that slack (C5 -1 %, A/B)
+                    if (!c.norm_zones) {
+                        if (rl) ladder();
+                        ladder_done = true;
+                    }
                     __syncthreads();
 #ifdef CN_STAMPS
                     const unsigned long long tl3 = clock64();
@@ -3351,7 +3361,7 @@ __global__ void __launch_bounds__(CN_BLK, 3) cn_step_kernel(StepArgs g, cn_confi
             human_post(tid, nvx, nvy, path_vr(tid));
         }
         STAMP_T(21, 64);
-        if (rl) ladder();
+        if (rl && !ladder_done) ladder();
         STAMP_T(20, 64);
     }
     __syncthreads();
